@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/*.json from the REFERENCE ec-cpp (oracle/_ref).
+
+Run in the build container (needs /root/reference):  python tests/golden/make_golden.py
+
+* tables.json  : SHA-256 of LOG / EXP / LOG_WALSH as held by the reference's
+                 golden header include/ec-cpp/table_f2e16.hpp (parsed here as
+                 data), of the tables ec-cpp builds at run time, and of the
+                 65,535 AFFT skews (pinned in the reference by
+                 test/erasure_coding/reconstruct.cpp:211-225).
+* vectors.json : encode / reconstruct / reconstruct_from_systematic outputs of
+                 ec-cpp on seeded synthetic payloads (erasure-coding-crust_amd/synth.py)
+                 and on the reference tests' own known-answer strings
+                 (test/erasure_coding/reconstruct.cpp:16-18,41-46,59-66,507-512).
+                 Small outputs are stored in hex, large ones as SHA-256.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import re
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "erasure-coding-crust_amd"))
+import oracle as orc  # noqa: E402
+import synth  # noqa: E402
+
+REF_TABLE_HDR = "/root/reference/include/ec-cpp/table_f2e16.hpp"
+OUT = os.path.dirname(os.path.abspath(__file__))
+HEX_LIMIT = 4096
+
+# the reference tests' payload strings (reconstruct.cpp:16-18, 41-46, 59-66)
+TEST_DATA = ("This is a test string. The purpose of it is not allow the evil forces to "
+             "conquer the world!!")
+LONG_DATA = ("wasioghowerhqht87y450t984y1h5oh243ptgwfhyqa9wyf9 yu9y9r "
+             "239y509y23trhr8247y p1qut59 2914tu520 t589u3t9y7u32w9ty 89qewy923u5 "
+             "h4123hty t90y1982u95yu "
+             "91259oy92y5tr90oweiovfdkljscnvkljasnhiewytr9q8uj5toinh1 "
+             "l;n4ou98uiqwp2j3mrtlknmeswlkjf p9o87q90p u2p45j243o56u9uyew98fuqw")
+
+
+def sha(b: bytes) -> str:
+    return hashlib.sha256(b).hexdigest()
+
+
+def parse_header_tables():
+    txt = open(REF_TABLE_HDR).read()
+    out = {}
+    for name in ("LOG_TABLE", "EXP_TABLE", "LOG_WALSH"):
+        m = re.search(name + r"\[\]\s*=\s*\{(.*?)\};", txt, re.S)
+        nums = [int(x) for x in re.findall(r"\d+", re.sub(r"Multiplier", "", m.group(1)))]
+        out[name] = np.array(nums, dtype=np.uint16)
+    return out
+
+
+def payload_from_spec(spec) -> bytes:
+    kind = spec["kind"]
+    if kind == "text":
+        return spec["text"].encode()
+    if kind == "splitmix":
+        return synth.payload(spec["seed"], spec["len"]).tobytes()
+    if kind == "mod255":
+        return synth.pattern_mod255(spec["len"]).tobytes()
+    if kind == "alpha24":
+        return synth.pattern_alpha24(spec["len"]).tobytes()
+    raise ValueError(kind)
+
+
+def present_from_spec(nv, k, thr, spec):
+    if spec == "all":
+        return list(range(nv))
+    if isinstance(spec, dict):
+        cnt = {"k": k, "threshold": thr}.get(spec["count"], spec["count"])
+        return [int(x) for x in synth.present_set(spec["seed"], nv, cnt)]
+    return list(spec)
+
+
+def blob(b: bytes, key: str, d: dict):
+    d[key + "_sha256"] = sha(b)
+    d[key + "_len"] = len(b)
+    if len(b) <= HEX_LIMIT:
+        d[key + "_hex"] = b.hex()
+
+
+def main():
+    ref = orc.RefEC()
+    log, exp, lw = ref.tables()
+    hdr = parse_header_tables()
+    tables = {
+        "source": "include/ec-cpp/table_f2e16.hpp (golden) and ec-cpp run-time tables",
+        "header_LOG_TABLE_sha256": sha(hdr["LOG_TABLE"].tobytes()),
+        "header_EXP_TABLE_sha256": sha(hdr["EXP_TABLE"].tobytes()),
+        "header_LOG_WALSH_sha256": sha(hdr["LOG_WALSH"].tobytes()),
+        "runtime_log_sha256": sha(log.tobytes()),
+        "runtime_exp_sha256": sha(exp.tobytes()),
+        "runtime_log_walsh_sha256": sha(lw.tobytes()),
+        "skews_sha256": sha(ref.skews().tobytes()),
+        "samples": {
+            "log": {str(i): int(log[i]) for i in (0, 1, 2, 3, 255, 256, 65535)},
+            "exp": {str(i): int(exp[i]) for i in (0, 1, 2, 3, 255, 256, 65534, 65535)},
+            "log_walsh": {str(i): int(lw[i]) for i in (0, 1, 2, 3, 65535)},
+            "skews": {str(i): int(v) for i, v in enumerate(ref.skews()[:32])},
+        },
+    }
+    assert (hdr["LOG_TABLE"] == log).all() and (hdr["EXP_TABLE"] == exp).all()
+    assert (hdr["LOG_WALSH"] == lw).all()
+    json.dump(tables, open(os.path.join(OUT, "tables.json"), "w"), indent=1)
+
+    cases = []
+    # --- reference known-answer payloads at n_validators = 6 (reconstruct.cpp:19)
+    for name, text in (("test_data", TEST_DATA), ("long_data", LONG_DATA), ("one", "1"),
+                       ("test_data_bench", TEST_DATA[:-1])):
+        for present in ("all", [0, 1], [1, 5], [2, 3, 4, 5], [2, 5], [0, 1, 2, 3]):
+            cases.append({"nv": 6, "payload": {"kind": "text", "text": text},
+                          "present": present, "tag": f"kat:{name}"})
+    cases.append({"nv": 6, "payload": {"kind": "mod255", "len": 1 << 20}, "present": "all",
+                  "tag": "kat:Cpp_Decode_Big"})
+    cases.append({"nv": 2, "payload": {"kind": "text", "text": LONG_DATA}, "present": "all",
+                  "tag": "kat:Cpp_Create"})
+    # --- seeded synthetic sweep
+    seed = 0
+    for nv in (2, 3, 4, 5, 6, 7, 8, 9, 31, 100, 257, 1000, 1023, 1024, 1025):
+        for plen in (1, 2, 3, 15, 92, 300, 511, 512, 513, 3001, 5000):
+            for pres in ("all", {"count": "k", "seed": 10**6 + seed},
+                         {"count": "threshold", "seed": 2 * 10**6 + seed}):
+                cases.append({"nv": nv, "payload": {"kind": "splitmix", "seed": seed, "len": plen},
+                              "present": pres, "tag": "sweep"})
+            seed += 1
+    # --- BASELINE.json configs (sizes the CPU oracle finishes in seconds)
+    for nv, plen, pres in (
+            (1024, 300, "all"),                                            # config 1
+            (6, 300, "all"),
+            (1024, 1_000_000, {"count": "threshold", "seed": 10**6}),      # config 2
+            (1024, 1_000_000, {"count": "k", "seed": 10**6 + 1}),
+            (1024, 100_000, {"count": "threshold", "seed": 10**6 + 2}),
+            (4096, 1_000_000, {"count": "threshold", "seed": 10**6 + 3}),  # config 4 shape
+            (4096, 5000, {"count": "k", "seed": 10**6 + 4}),
+            (65536, 1, {"count": "k", "seed": 10**6 + 5}),
+            (65536, 70_000, {"count": "threshold", "seed": 10**6 + 6}),
+            (1024, 10_000_000, {"count": "threshold", "seed": 10**6 + 7})):  # config 3
+        cases.append({"nv": nv, "payload": {"kind": "splitmix", "seed": 7000 + plen % 997, "len": plen},
+                      "present": pres, "tag": "config"})
+    cases.append({"nv": 1024, "payload": {"kind": "mod255", "len": 1_000_000},
+                  "present": {"count": "threshold", "seed": 10**6 + 8}, "tag": "config:mod255"})
+    cases.append({"nv": 1024, "payload": {"kind": "alpha24", "len": 300}, "present": "all",
+                  "tag": "config:alpha24"})
+
+    out_cases = []
+    for c in cases:
+        nv = c["nv"]
+        p = payload_from_spec(c["payload"])
+        n, k = ref.params(nv)
+        thr = ref.threshold(nv)
+        shards = ref.encode(nv, p)
+        present = present_from_spec(nv, k, thr, c["present"])
+        pres = set(present)
+        rec = ref.reconstruct(nv, [shards[i] if i in pres else None for i in range(nv)])
+        d = dict(c)
+        d.update({"n": n, "k": k, "threshold": thr, "payload_len": len(p),
+                  "shard_len": len(shards[0])})
+        blob(b"".join(shards), "shards", d)
+        blob(rec, "reconstructed", d)
+        assert rec[: len(p)] == p
+        if c["present"] == "all" or all(i in pres for i in range(k)):
+            sysout = ref.reconstruct_from_systematic(nv, shards[:k])
+            blob(sysout, "systematic", d)
+        out_cases.append(d)
+        print(c["tag"], nv, len(p), file=sys.stderr)
+
+    json.dump({"generator": "tests/golden/make_golden.py", "cases": out_cases},
+              open(os.path.join(OUT, "vectors.json"), "w"), indent=0)
+
+
+if __name__ == "__main__":
+    main()
