@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Device-resident encode+reconstruct throughput (BASELINE.json metric).
+
+One step = for a batch of independent payloads already resident in HBM:
+  ECCR_AMD_encode_batch   (payload -> n_validators shards, ec-cpp encode)
+  ECCR_AMD_error_locator  (per-payload erasure pattern -> log multipliers)
+  ECCR_AMD_reconstruct_batch (random `threshold`-of-n shards -> payload)
+value = total payload bytes of all ranks / max-over-ranks step time, GiB/s.
+
+Multi-GPU: one process per GPU (torchrun), payloads sharded by rank with no
+data-path collective (weak scaling); RCCL only for the barrier / max-timing.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with a
+`roofline` object for the dominant kernel (HIP events on the launch stream)
+and a `cpu_baseline` timed on this host (the reference ec-cpp built in
+oracle/_ref if present, else the C restatement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "erasure-coding-crust_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import ecc_amd as E  # noqa: E402
+import synth  # noqa: E402
+
+METRIC = "device-resident encode+reconstruct GiB/s (and % HBM roofline), n_val=1024"
+HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def cpu_baseline(nv, plen, cnt, seconds):
+    """Single-thread CPU rate of the same path on a bounded sample."""
+    import oracle as orc
+    kind = "reference" if orc.RefEC.available() else "port"
+    impl = orc.RefEC() if kind == "reference" else orc.Oracle()
+    n, k = impl.params(nv)
+    p = synth.payload(424242, plen).tobytes()
+    present = synth.present_mask(10**6, nv, cnt)
+    t_enc = t_dec = 0.0
+    reps = 0
+    t_start = time.perf_counter()
+    while reps < 1 or time.perf_counter() - t_start < seconds:
+        if kind == "reference":
+            te, td = impl.time(nv, p, present)
+        else:
+            t0 = time.perf_counter()
+            sh = impl.encode(nv, p)
+            t1 = time.perf_counter()
+            impl.reconstruct(nv, [sh[i] if present[i] else None for i in range(nv)])
+            te, td = t1 - t0, time.perf_counter() - t1
+        t_enc += te
+        t_dec += td
+        reps += 1
+    gib = reps * plen / (t_enc + t_dec) / 2**30
+    return {"value": round(gib, 6), "unit": "GiB/s", "cores": 1, "kind": kind,
+            "sample": f"{reps} x ({plen} B payload encode + reconstruct from {cnt} of {nv} "
+                      f"shards), 1 thread, {'ec-cpp -O3 (oracle/_ref)' if kind == 'reference' else 'oracle/ec_oracle.c'}",
+            "encode_GiBps": round(reps * plen / t_enc / 2**30, 6),
+            "reconstruct_GiBps": round(reps * plen / t_dec / 2**30, 6)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=4096, help="payloads per GPU")
+    ap.add_argument("--payload", type=int, default=1_000_000)
+    ap.add_argument("--nv", type=int, default=1024)
+    ap.add_argument("--present", default="threshold", help="'threshold', 'k' or a count")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    assert E.lib().ECCR_AMD_init_device().tag == 0, E.last_error()
+
+    nv, plen, B = args.nv, args.payload, args.batch
+    n, k, thr = E.code_params(nv)
+    cnt = {"threshold": thr, "k": k}.get(args.present) or int(args.present)
+    sl = E.shard_len(nv, plen)
+    dev = torch.device("cuda", local)
+
+    # synthetic inputs, resident before timing; seeds are global payload indices
+    seeds = [rank * B + b for b in range(B)]
+    d_pay = torch.empty((B, plen), dtype=torch.uint8, device=dev)
+    for c0 in range(0, B, 256):
+        d_pay[c0:c0 + 256] = synth.payloads_torch(seeds[c0:c0 + 256], plen, device=dev)
+    d_pres = torch.from_numpy(synth.present_masks([10**6 + s for s in seeds], nv, cnt, n)).to(dev)
+    d_sh = torch.empty((B, nv, sl), dtype=torch.uint8, device=dev)
+    d_el = torch.empty((B, n), dtype=torch.int16, device=dev)
+    d_out = torch.empty((B, sl * k), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    ev = []
+
+    def step(record):
+        if record:
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            e[0].record(stream)
+        E.encode_batch(nv, d_pay, plen, plen, B, d_sh, sl, stream)
+        if record:
+            e[1].record(stream)
+        E.error_locator(nv, d_pres, B, d_el, stream)
+        if record:
+            e[2].record(stream)
+        E.reconstruct_batch(nv, d_sh, sl, sl, d_pres, d_el, B, d_out, sl * k, stream)
+        if record:
+            e[3].record(stream)
+            ev.append(e)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # sanity: the last step's reconstruction equals the payloads (round trip)
+    ok = bool(torch.equal(d_out[:, :plen], d_pay))
+
+    ms = lambda a, b: np.mean([x[a].elapsed_time(x[b]) for x in ev])  # noqa: E731
+    t_enc, t_loc, t_rec = ms(0, 1), ms(1, 2), ms(2, 3)
+    enc_bytes = B * (plen + nv * sl)           # SURVEY.md §8d algorithmic bytes
+    rec_bytes = B * (cnt + k) * sl + B * n * 2  # + error-locator multipliers read
+    kern = {"encode": (t_enc, enc_bytes), "reconstruct": (t_rec, rec_bytes)}
+    dom = max(kern, key=lambda x: kern[x][0])
+    t_dom, b_dom = kern[dom]
+    achieved = b_dom / (t_dom * 1e-3)
+
+    total_bytes = world * B * plen * args.steps
+    value = total_bytes / elapsed / 2**30
+    line = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u16",
+        "data": "synthetic: splitmix64 payloads (seed = payload index), per-payload random "
+                f"{cnt}-of-{nv} present shards",
+        "config": {"workload": f"config2: {plen} B payloads, n_validators={nv}, batch={B}/GPU, "
+                               f"encode + reconstruct from {cnt} random shards",
+                   "n_validators": nv, "payload_bytes": plen, "batch_per_gpu": B,
+                   "present_shards": cnt, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved / 1e9, 2),
+                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
+                     "traffic": None, "bytes_per_launch": b_dom, "avg_launch_ms": round(t_dom, 4)},
+        "kernels_ms": {"encode": round(t_enc, 4), "error_locator": round(t_loc, 4),
+                       "reconstruct": round(t_rec, 4)},
+        "encode_GiBps": round(world * B * plen / (t_enc * 1e-3) / 2**30, 3),
+        "reconstruct_GiBps": round(world * B * plen / ((t_loc + t_rec) * 1e-3) / 2**30, 3),
+        "roundtrip_ok": ok,
+    }
+    if rank == 0:
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(nv, plen, cnt, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

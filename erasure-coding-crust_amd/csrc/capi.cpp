@@ -1,0 +1,414 @@
+// capi.cpp — the erasure_coding.h C ABI (src/erasure_coding.rs of the
+// reference) plus the ec_amd.h device-batch extension, on the HIP path.
+//
+// Validation order and error mapping follow src/erasure_coding.rs; the codec
+// results follow ec-cpp (include/ec-cpp/reed-solomon.hpp).  Deliberate
+// divergence: where the Rust layer panics (null/empty payload, null out
+// pointers) we return NPRS_RESULT_BAD_PAYLOAD / abort with a message.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/erasure_coding/ec_amd.h"
+#include "../../include/erasure_coding/erasure_coding.h"
+#include "ec_kernels.hpp"
+#include "ec_runtime.hpp"
+#include "gf_field.hpp"
+
+using namespace ecamd;
+
+namespace {
+
+NPRSResult result(NPRSResult_Tag tag) {
+  NPRSResult r;
+  std::memset(&r, 0, sizeof r);
+  r.tag = tag;
+  return r;
+}
+
+[[noreturn]] void contract_violation(const char *what) {  // Rust assert! == abort
+  std::fprintf(stderr, "erasure_coding_crust(amd): contract violation: %s\n", what);
+  std::abort();
+}
+
+// src/erasure_coding.rs:70-98 (recovery_threshold + code_params)
+NPRSResult params_or_error(unsigned long nv, CodeParams *p) {
+  switch (code_params(nv, p)) {
+    case ParamError::kTooManyValidators: return result(NPRS_RESULT_TOO_MANY_VALIDATORS);
+    case ParamError::kNotEnoughValidators: return result(NPRS_RESULT_NOT_ENOUGH_VALIDATORS);
+    default: return result(NPRS_RESULT_OK);
+  }
+}
+
+bool hip_check(hipError_t e, const char *what) {
+  if (e == hipSuccess) return true;
+  set_error(std::string("erasure_coding_crust(amd): ") + what + ": " + hipGetErrorString(e));
+  return false;
+}
+
+// host -> device -> host encode of one payload into pinned h_out [nv][sl]
+bool encode_host(const CodeParams &p, const uint8_t *payload, size_t len, HostCtx *c,
+                 size_t *sl_out) {
+  DeviceState *d = device_state();
+  if (!d) return false;
+  const size_t sl = shard_len(p.k, len);
+  const size_t out_bytes = size_t(p.nv) * sl;
+  if (!ensure_host(&c->h_in, &c->h_in_cap, len) ||
+      !ensure_dev(reinterpret_cast<void **>(&c->d_in), &c->d_in_cap, len) ||
+      !ensure_host(&c->h_out, &c->h_out_cap, out_bytes) ||
+      !ensure_dev(reinterpret_cast<void **>(&c->d_out), &c->d_out_cap, out_bytes))
+    return false;
+  void *scratch = device_scratch(d, encode_scratch_bytes(p, len, 1));
+  std::memcpy(c->h_in, payload, len);
+  if (!hip_check(hipMemcpyAsync(c->d_in, c->h_in, len, hipMemcpyHostToDevice, c->stream), "H2D") ||
+      !hip_check(launch_encode(p, device_tables(d), c->d_in, len, len, 1, c->d_out, sl, scratch,
+                               c->stream),
+                 "encode launch") ||
+      !hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost, c->stream),
+                 "D2H") ||
+      !hip_check(hipStreamSynchronize(c->stream), "encode"))
+    return false;
+  *sl_out = sl;
+  return true;
+}
+
+// reconstruct from shards staged in c->h_in ([nv][sl], present[] flags) into c->h_out
+bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, size_t sl,
+                      HostCtx *c) {
+  DeviceState *d = device_state();
+  if (!d) return false;
+  const size_t in_bytes = size_t(p.nv) * sl, out_bytes = sl * p.k;
+  if (!ensure_dev(reinterpret_cast<void **>(&c->d_in), &c->d_in_cap, in_bytes) ||
+      !ensure_dev(reinterpret_cast<void **>(&c->d_out), &c->d_out_cap, out_bytes) ||
+      !ensure_host(&c->h_out, &c->h_out_cap, out_bytes) ||
+      !ensure_dev(reinterpret_cast<void **>(&c->d_present), &c->d_present_cap, p.n) ||
+      !ensure_dev(reinterpret_cast<void **>(&c->d_elog), &c->d_elog_cap, size_t(p.n) * 2))
+    return false;
+  bool all_systematic = true;
+  for (uint32_t y = 0; y < p.k; ++y) all_systematic &= present[y] != 0;
+  if (!hip_check(hipMemcpyAsync(c->d_in, c->h_in, in_bytes, hipMemcpyHostToDevice, c->stream),
+                 "H2D"))
+    return false;
+  if (all_systematic) {
+    // every systematic shard is present: decode == interleave (exact)
+    if (!hip_check(launch_systematic(p, c->d_in, sl, sl, 1, c->d_out, out_bytes, c->stream),
+                   "systematic launch"))
+      return false;
+  } else {
+    const uint16_t *fold = device_fold(d, p.n);
+    if (!fold) return false;
+    void *scratch = device_scratch(d, reconstruct_scratch_bytes(p, sl, 1));
+    if (!hip_check(hipMemcpyAsync(c->d_present, present.data(), p.n, hipMemcpyHostToDevice,
+                                  c->stream),
+                   "H2D present") ||
+        !hip_check(launch_error_locator(p, c->d_present, 1, fold, c->d_elog, nullptr, c->stream),
+                   "error locator launch") ||
+        !hip_check(launch_reconstruct(p, device_tables(d), c->d_in, sl, sl, c->d_present,
+                                      c->d_elog, 1, c->d_out, out_bytes, scratch, c->stream),
+                   "reconstruct launch"))
+      return false;
+  }
+  return hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost,
+                                  c->stream),
+                   "D2H") &&
+         hip_check(hipStreamSynchronize(c->stream), "reconstruct");
+}
+
+bool take_output(HostCtx *c, size_t bytes, DataBlock *out) {
+  uint8_t *buf = static_cast<uint8_t *>(std::malloc(bytes ? bytes : 1));
+  if (!buf) return false;
+  std::memcpy(buf, c->h_out, bytes);
+  out->array = buf;
+  out->length = bytes;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+NPRSResult ECCR_get_recovery_threshold(unsigned long nv, unsigned long *threshold_out) {
+  if (!threshold_out) contract_violation("threshold_out is null");
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag == NPRS_RESULT_OK) *threshold_out = p.threshold;
+  return r;
+}
+
+void ECCR_deallocate_data_block(DataBlock *data) {
+  if (!data || !data->array) contract_violation("deallocate_data_block: null");
+  std::free(data->array);
+  data->array = nullptr;
+  data->length = 0;
+}
+
+void ECCR_deallocate_chunk(Chunk *data) {
+  if (!data) contract_violation("deallocate_chunk: null");
+  ECCR_deallocate_data_block(&data->data);
+}
+
+void ECCR_deallocate_chunk_list(ChunksList *list) {
+  if (!list || !list->data) contract_violation("deallocate_chunk_list: null");
+  for (unsigned long i = 0; i < list->count; ++i) ECCR_deallocate_chunk(&list->data[i]);
+  std::free(list->data);
+  list->data = nullptr;
+  list->count = 0;
+}
+
+NPRSResult ECCR_AFFT_Table(uint16_t (*output)[65535]) {
+  if (!output) contract_violation("AFFT_Table: null");
+  std::memcpy(*output, field().skews.data(), 65535 * sizeof(uint16_t));
+  return result(NPRS_RESULT_OK);
+}
+
+NPRSResult ECCR_obtain_chunks(unsigned long nv, const DataBlock *message, ChunksList *output) {
+  if (!message || !output) contract_violation("obtain_chunks: null argument");
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag != NPRS_RESULT_OK) return r;
+  if (!message->array || message->length == 0) return result(NPRS_RESULT_BAD_PAYLOAD);
+  HostCtx *c = host_ctx();
+  size_t sl = 0;
+  if (!c || !encode_host(p, message->array, message->length, c, &sl))
+    return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+  Chunk *chunks = static_cast<Chunk *>(std::malloc(sizeof(Chunk) * nv));
+  if (!chunks) return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+  for (unsigned long v = 0; v < nv; ++v) {
+    uint8_t *b = static_cast<uint8_t *>(std::malloc(sl));
+    std::memcpy(b, c->h_out + v * sl, sl);
+    chunks[v].data.array = b;
+    chunks[v].data.length = sl;
+    chunks[v].index = v;
+  }
+  output->data = chunks;
+  output->count = nv;
+  return result(NPRS_RESULT_OK);
+}
+
+NPRSResult ECCR_reconstruct(unsigned long nv, const ChunksList *input, DataBlock *outdata) {
+  if (!outdata || !input || !input->data) contract_violation("reconstruct: null argument");
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag != NPRS_RESULT_OK) return r;
+  // src/erasure_coding.rs:363-387: first n_validators entries, positional
+  std::vector<const Chunk *> slot(nv, nullptr);
+  unsigned long sl = 0;
+  bool have_len = false;
+  const unsigned long take = input->count < nv ? input->count : nv;
+  for (unsigned long i = 0; i < take; ++i) {
+    const Chunk &ch = input->data[i];
+    if (ch.index >= nv) {
+      NPRSResult e = result(NPRS_RESULT_CHUNK_INDEX_OUT_OF_BOUNDS);
+      e.chunk_index_out_of_bounds.chunk_index = ch.index;
+      e.chunk_index_out_of_bounds.n_validators = nv;
+      return e;
+    }
+    if (!ch.data.array || ch.data.length == 0) continue;
+    if (!have_len) {
+      sl = ch.data.length;
+      have_len = true;
+    }
+    if (sl % 2 != 0) return result(NPRS_RESULT_UNEVEN_LENGTH);
+    if (sl != ch.data.length) return result(NPRS_RESULT_NON_UNIFORM_CHUNKS);
+    slot[ch.index] = &ch;
+  }
+  std::vector<uint8_t> present(p.n, 0);
+  uint32_t count = 0;
+  for (unsigned long v = 0; v < nv; ++v)
+    if (slot[v]) {
+      present[v] = 1;
+      ++count;
+    }
+  if (count < p.k) return result(NPRS_RESULT_NOT_ENOUGH_CHUNKS);  // reed-solomon.hpp:99-100
+  HostCtx *c = host_ctx();
+  if (!c || !ensure_host(&c->h_in, &c->h_in_cap, size_t(nv) * sl))
+    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  for (unsigned long v = 0; v < nv; ++v)
+    if (slot[v]) std::memcpy(c->h_in + v * sl, slot[v]->data.array, sl);
+  if (!reconstruct_host(p, present, sl, c) || !take_output(c, sl * p.k, outdata))
+    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  return result(NPRS_RESULT_OK);
+}
+
+NPRSResult ECCR_reconstruct_from_systematic(unsigned long nv, const ChunksList *input,
+                                            DataBlock *outdata) {
+  if (!outdata || !input || !input->data) contract_violation("systematic: null argument");
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag != NPRS_RESULT_OK) return r;
+  // src/erasure_coding.rs:291-312: chunks with index < k, all k required
+  std::vector<const Chunk *> slot(p.k, nullptr);
+  for (unsigned long i = 0; i < input->count; ++i) {
+    const Chunk &ch = input->data[i];
+    if (ch.index < p.k) slot[ch.index] = &ch;
+  }
+  for (uint32_t y = 0; y < p.k; ++y)
+    if (!slot[y]) return result(NPRS_RESULT_NOT_ENOUGH_CHUNKS);
+  // reed-solomon.hpp:155-165: first shard sets the length; empty -> error
+  const unsigned long sl = slot[0]->data.array ? slot[0]->data.length : 0;
+  if (sl / 2 == 0) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);  // kEmptyShard
+  for (uint32_t y = 0; y < p.k; ++y) {
+    const unsigned long l = slot[y]->data.array ? slot[y]->data.length : 0;
+    if (l / 2 != sl / 2) return result(NPRS_RESULT_NON_UNIFORM_CHUNKS);
+  }
+  const size_t used = sl / 2 * 2;
+  HostCtx *c = host_ctx();
+  DeviceState *d = c ? device_state() : nullptr;
+  const size_t in_bytes = size_t(p.k) * used, out_bytes = used * p.k;
+  if (!c || !d || !ensure_host(&c->h_in, &c->h_in_cap, in_bytes) ||
+      !ensure_host(&c->h_out, &c->h_out_cap, out_bytes) ||
+      !ensure_dev(reinterpret_cast<void **>(&c->d_in), &c->d_in_cap, in_bytes) ||
+      !ensure_dev(reinterpret_cast<void **>(&c->d_out), &c->d_out_cap, out_bytes))
+    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  for (uint32_t y = 0; y < p.k; ++y) std::memcpy(c->h_in + y * used, slot[y]->data.array, used);
+  CodeParams pk = p;
+  pk.nv = p.k;  // staged layout holds only the k systematic shards
+  if (!hip_check(hipMemcpyAsync(c->d_in, c->h_in, in_bytes, hipMemcpyHostToDevice, c->stream),
+                 "H2D") ||
+      !hip_check(launch_systematic(pk, c->d_in, used, used, 1, c->d_out, out_bytes, c->stream),
+                 "systematic launch") ||
+      !hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost, c->stream),
+                 "D2H") ||
+      !hip_check(hipStreamSynchronize(c->stream), "systematic") ||
+      !take_output(c, out_bytes, outdata))
+    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  return result(NPRS_RESULT_OK);
+}
+
+NPRSResult ECCR_Test_MeasurePerformance(const DataBlock *message, unsigned long nv,
+                                        unsigned long *us_enc, unsigned long *us_dec) {
+  if (!message) return result(NPRS_RESULT_BAD_PAYLOAD);
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag != NPRS_RESULT_OK) return r;
+  if (!message->array || message->length == 0) return result(NPRS_RESULT_BAD_PAYLOAD);
+  HostCtx *c = host_ctx();
+  if (!c) return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+  using clk = std::chrono::steady_clock;
+  size_t sl = 0;
+  const auto t0 = clk::now();
+  if (!encode_host(p, message->array, message->length, c, &sl))
+    return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+  const auto t1 = clk::now();
+  // reconstruct from all shards (src/erasure_coding.rs:200-211)
+  if (!ensure_host(&c->h_in, &c->h_in_cap, size_t(nv) * sl))
+    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  std::memcpy(c->h_in, c->h_out, size_t(nv) * sl);
+  std::vector<uint8_t> present(p.n, 0);
+  for (unsigned long v = 0; v < nv; ++v) present[v] = 1;
+  const auto t2 = clk::now();
+  if (!reconstruct_host(p, present, sl, c)) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  const auto t3 = clk::now();
+  if (us_enc)
+    *us_enc = (unsigned long)std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
+  if (us_dec)
+    *us_dec = (unsigned long)std::chrono::duration_cast<std::chrono::microseconds>(t3 - t2).count();
+  return result(NPRS_RESULT_OK);
+}
+
+// ------------------------------------------------------------- ec_amd.h --
+
+NPRSResult ECCR_AMD_code_params(unsigned long nv, unsigned long *n, unsigned long *k,
+                                unsigned long *thr) {
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag != NPRS_RESULT_OK) return r;
+  if (n) *n = p.n;
+  if (k) *k = p.k;
+  if (thr) *thr = p.threshold;
+  return r;
+}
+
+unsigned long ECCR_AMD_shard_len(unsigned long nv, unsigned long plen) {
+  CodeParams p;
+  if (code_params(nv, &p) != ParamError::kOk) return 0;
+  return shard_len(p.k, plen);
+}
+
+int ECCR_AMD_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+NPRSResult ECCR_AMD_init_device(void) {
+  return device_state() ? result(NPRS_RESULT_OK) : result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+}
+
+NPRSResult ECCR_AMD_encode_batch(unsigned long nv, const uint8_t *d_payloads, unsigned long plen,
+                                 unsigned long pstride, unsigned long batch, uint8_t *d_shards,
+                                 unsigned long sstride, void *stream) {
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag != NPRS_RESULT_OK) return r;
+  if (plen == 0) return result(NPRS_RESULT_BAD_PAYLOAD);
+  if (sstride < shard_len(p.k, plen) || pstride < plen) return result(NPRS_RESULT_BAD_PAYLOAD);
+  DeviceState *d = device_state();
+  if (!d) return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+  void *scratch = device_scratch(d, encode_scratch_bytes(p, plen, batch));
+  if (!hip_check(launch_encode(p, device_tables(d), d_payloads, plen, pstride, batch, d_shards,
+                               sstride, scratch, static_cast<hipStream_t>(stream)),
+                 "encode launch"))
+    return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+  return result(NPRS_RESULT_OK);
+}
+
+NPRSResult ECCR_AMD_error_locator(unsigned long nv, const uint8_t *d_present, unsigned long batch,
+                                  uint16_t *d_err_log, void *stream) {
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag != NPRS_RESULT_OK) return r;
+  DeviceState *d = device_state();
+  const uint16_t *fold = d ? device_fold(d, p.n) : nullptr;
+  if (!fold) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  if (!hip_check(launch_error_locator(p, d_present, batch, fold, d_err_log, nullptr,
+                                      static_cast<hipStream_t>(stream)),
+                 "error locator launch"))
+    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  return result(NPRS_RESULT_OK);
+}
+
+NPRSResult ECCR_AMD_reconstruct_batch(unsigned long nv, const uint8_t *d_shards,
+                                      unsigned long slen, unsigned long sstride,
+                                      const uint8_t *d_present, const uint16_t *d_err_log,
+                                      unsigned long batch, uint8_t *d_out,
+                                      unsigned long ostride, void *stream) {
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag != NPRS_RESULT_OK) return r;
+  if (slen % 2 != 0) return result(NPRS_RESULT_UNEVEN_LENGTH);
+  if (sstride < slen || ostride < slen * p.k) return result(NPRS_RESULT_NON_UNIFORM_CHUNKS);
+  DeviceState *d = device_state();
+  if (!d) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  void *scratch = device_scratch(d, reconstruct_scratch_bytes(p, slen, batch));
+  if (!hip_check(launch_reconstruct(p, device_tables(d), d_shards, slen, sstride, d_present,
+                                    d_err_log, batch, d_out, ostride, scratch,
+                                    static_cast<hipStream_t>(stream)),
+                 "reconstruct launch"))
+    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  return result(NPRS_RESULT_OK);
+}
+
+NPRSResult ECCR_AMD_systematic_batch(unsigned long nv, const uint8_t *d_shards, unsigned long slen,
+                                     unsigned long sstride, unsigned long batch, uint8_t *d_out,
+                                     unsigned long ostride, void *stream) {
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag != NPRS_RESULT_OK) return r;
+  if (sstride < slen || ostride < slen / 2 * 2 * p.k) return result(NPRS_RESULT_NON_UNIFORM_CHUNKS);
+  if (!device_state()) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  if (!hip_check(launch_systematic(p, d_shards, slen / 2 * 2, sstride, batch, d_out, ostride,
+                                   static_cast<hipStream_t>(stream)),
+                 "systematic launch"))
+    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  return result(NPRS_RESULT_OK);
+}
+
+const char *ECCR_AMD_last_error(void) { return last_error(); }
+
+}  // extern "C"

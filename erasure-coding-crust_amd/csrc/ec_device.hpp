@@ -1,0 +1,64 @@
+// ec_device.hpp — CDNA4 device arithmetic for the NPB codec.
+//
+// Byte-planar symbols: one uint2 {l, h} holds 4 GF(2^16) symbols (4 pieces or
+// 4 shard positions); l has their low bytes, h their high bytes.  A multiply
+// by a log-domain constant c is a GF(2)-linear map, so
+//     x * c = XOR_g T_g[group_g(x)]
+// over 3-bit (and 2-bit) bit groups of x.  Each T_g lookup of 4 symbols at
+// once is one v_perm_b32 (8-entry byte table held in two registers, selector
+// bytes = the 4 group values), i.e. 12 v_perm + 6 selector masks + 6 v_bitop3
+// per 4 multiply-accumulates.  No LOG/EXP gathers, no LDS bank conflicts.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gf_field.hpp"
+
+namespace ecamd {
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ uint32_t vperm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+struct Tab {
+  uint32_t t[20];
+};
+
+__device__ __forceinline__ void load_tab(const MulTab *__restrict__ mt, uint32_t c, Tab &T) {
+  const uint4 *p = reinterpret_cast<const uint4 *>(mt + c);
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const uint4 v = p[q];
+    T.t[4 * q + 0] = v.x;
+    T.t[4 * q + 1] = v.y;
+    T.t[4 * q + 2] = v.z;
+    T.t[4 * q + 3] = v.w;
+  }
+}
+
+// (yl, yh) ^= (xl, xh) * c, four symbols at once
+__device__ __forceinline__ void mul_acc(uint32_t xl, uint32_t xh, const Tab &T, uint32_t &yl,
+                                        uint32_t &yh) {
+  const uint32_t s0 = xl & 0x07070707u;
+  const uint32_t s1 = (xl >> 3) & 0x07070707u;
+  const uint32_t s2 = (xl >> 6) & 0x03030303u;
+  const uint32_t s3 = xh & 0x07070707u;
+  const uint32_t s4 = (xh >> 3) & 0x07070707u;
+  const uint32_t s5 = (xh >> 6) & 0x03030303u;
+  uint32_t l = xor3(yl, vperm(T.t[1], T.t[0], s0), vperm(T.t[5], T.t[4], s1));
+  l = xor3(l, vperm(T.t[9], T.t[8], s3), vperm(T.t[13], T.t[12], s4));
+  l = xor3(l, vperm(T.t[16], T.t[16], s2), vperm(T.t[18], T.t[18], s5));
+  uint32_t h = xor3(yh, vperm(T.t[3], T.t[2], s0), vperm(T.t[7], T.t[6], s1));
+  h = xor3(h, vperm(T.t[11], T.t[10], s3), vperm(T.t[15], T.t[14], s4));
+  h = xor3(h, vperm(T.t[17], T.t[17], s2), vperm(T.t[19], T.t[19], s5));
+  yl = l;
+  yh = h;
+}
+
+}  // namespace ecamd

@@ -1,0 +1,378 @@
+// ec_kernels.hip — HIP kernels for gfx950: NPB Reed-Solomon encode, erasure
+// locator, reconstruct, systematic reconstruct.
+//
+// Generic path ("g" kernels): one workgroup owns G byte-planar groups (4 pieces
+// or 4 shard positions each) and runs the additive FFT stage by stage on a
+// [position][group] uint2 array in LDS (or global scratch for FFTs above
+// 4096 points).  Butterflies follow additive_fft.hpp:99-141 exactly; the
+// multiply is the v_perm lookup of ec_device.hpp.
+#include <hip/hip_runtime.h>
+
+#include "ec_device.hpp"
+#include "ec_kernels.hpp"
+
+namespace ecamd {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kLdsSlots = 4096;  // uint2 slots per buffer in LDS (32 KiB)
+
+__device__ __forceinline__ void ld(uint2 *p, uint32_t &l, uint32_t &h) {
+  const uint2 v = *p;
+  l = v.x;
+  h = v.y;
+}
+
+// inverse_afft (additive_fft.hpp:99-119) on S[pos * G + g], pos < 2^logsz
+__device__ void ifft_g(uint2 *S, int logG, int logsz, uint32_t index, const DevTables t) {
+  const int G = 1 << logG;
+  const int half = (1 << logsz) >> 1;
+  for (int m = 0; m < logsz; ++m) {
+    const int d = 1 << m;
+    for (int b = threadIdx.x; b < half * G; b += blockDim.x) {
+      const int g = b & (G - 1), pi = b >> logG;
+      const int i = ((pi >> m) << (m + 1)) | (pi & (d - 1));
+      const int j = (i & ~(2 * d - 1)) | d;
+      Tab T;
+      load_tab(t.mtab, t.skews[j - 1 + index], T);
+      uint32_t al, ah, bl, bh;
+      ld(S + i * G + g, al, ah);
+      ld(S + (i + d) * G + g, bl, bh);
+      bl ^= al;
+      bh ^= ah;
+      mul_acc(bl, bh, T, al, ah);
+      S[i * G + g] = make_uint2(al, ah);
+      S[(i + d) * G + g] = make_uint2(bl, bh);
+    }
+    __syncthreads();
+  }
+}
+
+// afft (additive_fft.hpp:121-141)
+__device__ void fft_g(uint2 *S, int logG, int logsz, uint32_t index, const DevTables t) {
+  const int G = 1 << logG;
+  const int half = (1 << logsz) >> 1;
+  for (int m = logsz - 1; m >= 0; --m) {
+    const int d = 1 << m;
+    for (int b = threadIdx.x; b < half * G; b += blockDim.x) {
+      const int g = b & (G - 1), pi = b >> logG;
+      const int i = ((pi >> m) << (m + 1)) | (pi & (d - 1));
+      const int j = (i & ~(2 * d - 1)) | d;
+      Tab T;
+      load_tab(t.mtab, t.skews[j - 1 + index], T);
+      uint32_t al, ah, bl, bh;
+      ld(S + i * G + g, al, ah);
+      ld(S + (i + d) * G + g, bl, bh);
+      mul_acc(bl, bh, T, al, ah);
+      bl ^= al;
+      bh ^= ah;
+      S[i * G + g] = make_uint2(al, ah);
+      S[(i + d) * G + g] = make_uint2(bl, bh);
+    }
+    __syncthreads();
+  }
+}
+
+// reed-solomon.hpp:47-81 + poly_encoder.hpp:31-86,217-240 for 4*G pieces
+__global__ void __launch_bounds__(kBlock) encode_g(const uint8_t *__restrict__ payloads,
+                                                   uint64_t plen, uint64_t pstride,
+                                                   uint8_t *__restrict__ shards, uint64_t slen,
+                                                   uint64_t sstride, int nv, int logn, int logk,
+                                                   int logG, DevTables t, uint2 *scratch) {
+  extern __shared__ __attribute__((aligned(16))) uint2 smem[];
+  const int k = 1 << logk, n = 1 << logn, G = 1 << logG;
+  const uint64_t npieces = slen / 2;
+  const uint64_t piece0 = uint64_t(blockIdx.x) * 4 * G;
+  const uint8_t *P = payloads + uint64_t(blockIdx.y) * pstride;
+  uint8_t *SH = shards + uint64_t(blockIdx.y) * nv * sstride;
+  uint2 *S = smem, *Cf = smem + size_t(k) * G;
+  if (scratch) {
+    S = scratch + (uint64_t(blockIdx.y) * gridDim.x + blockIdx.x) * 2 * uint64_t(k) * G;
+    Cf = S + size_t(k) * G;
+  }
+  // BE-unpack 4 pieces per group, zero-padded (poly_encoder.hpp:53-76); the
+  // systematic shards are the data symbols themselves (poly_encoder.hpp:239)
+  for (int e = threadIdx.x; e < k * G; e += blockDim.x) {
+    const int g = e & (G - 1), i = e >> logG;
+    uint32_t xl = 0, xh = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint64_t p = piece0 + 4 * g + q;
+      const uint64_t off = p * 2 * uint64_t(k) + 2 * uint64_t(i);
+      const uint32_t hi = off < plen ? P[off] : 0;
+      const uint32_t lo = off + 1 < plen ? P[off + 1] : 0;
+      xl |= lo << (8 * q);
+      xh |= hi << (8 * q);
+      if (p < npieces) {
+        SH[uint64_t(i) * sstride + 2 * p] = uint8_t(hi);
+        SH[uint64_t(i) * sstride + 2 * p + 1] = uint8_t(lo);
+      }
+    }
+    S[e] = make_uint2(xl, xh);
+  }
+  __syncthreads();
+  ifft_g(S, logG, logk, 0, t);
+  for (int e = threadIdx.x; e < k * G; e += blockDim.x) Cf[e] = S[e];
+  __syncthreads();
+  for (int s = k; s < n && s < nv; s += k) {
+    if (s > k) {
+      for (int e = threadIdx.x; e < k * G; e += blockDim.x) S[e] = Cf[e];
+      __syncthreads();
+    }
+    fft_g(S, logG, logk, uint32_t(s), t);
+    for (int e = threadIdx.x; e < k * G; e += blockDim.x) {
+      const int g = e & (G - 1), v = s + (e >> logG);
+      if (v >= nv) continue;
+      const uint2 x = S[e];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t p = piece0 + 4 * g + q;
+        if (p < npieces) {
+          SH[uint64_t(v) * sstride + 2 * p] = uint8_t(x.y >> (8 * q));
+          SH[uint64_t(v) * sstride + 2 * p + 1] = uint8_t(x.x >> (8 * q));
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// poly_encoder.hpp:90-116 in the folded n-point form: one
+// workgroup per erasure pattern.  W lives in LDS (n <= 65536 -> 128 KiB) or
+// in global scratch.
+__global__ void __launch_bounds__(kBlock) error_locator_g(const uint8_t *__restrict__ present,
+                                                          int nv, int logn,
+                                                          const uint16_t *__restrict__ fold,
+                                                          uint16_t *__restrict__ elog,
+                                                          uint16_t *scratch) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t w16[];
+  const int n = 1 << logn;
+  const uint8_t *pr = present + uint64_t(blockIdx.x) * n;
+  uint16_t *W = scratch ? scratch + uint64_t(blockIdx.x) * n : w16;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) W[i] = (i < nv && pr[i]) ? 0 : 1;
+  __syncthreads();
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int h = 1; h < n; h <<= 1) {  // walsh.hpp:15-39
+      for (int b = threadIdx.x; b < n / 2; b += blockDim.x) {
+        const int i = (b / h) * 2 * h + (b % h);
+        const uint32_t x = W[i], y = W[i + h];
+        const uint32_t s = x + y, u = x + 65535u - y;
+        W[i] = uint16_t((s & 0xffff) + (s >> 16));
+        W[i + h] = uint16_t((u & 0xffff) + (u >> 16));
+      }
+      __syncthreads();
+    }
+    if (pass == 0) {
+      for (int i = threadIdx.x; i < n; i += blockDim.x)
+        W[i] = uint16_t((uint32_t(W[i]) * fold[i]) % 65535u);
+      __syncthreads();
+    }
+  }
+  uint16_t *E = elog + uint64_t(blockIdx.x) * n;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const bool erased = !(i < nv && pr[i]);
+    E[i] = erased ? uint16_t(65535u - W[i]) : W[i];
+  }
+}
+
+__device__ __forceinline__ uint32_t mul_index(uint32_t log_c) {  // 65535 == 0 (mod 65535)
+  return log_c == 65535u ? 0u : log_c;
+}
+
+// reed-solomon.hpp:83-134 + poly_encoder.hpp:118-215 for 4*G shard positions
+__global__ void __launch_bounds__(kBlock) reconstruct_g(
+    const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
+    const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
+    uint8_t *__restrict__ out, uint64_t ostride, int nv, int logn, int logk, int logG,
+    DevTables t, uint2 *scratch) {
+  extern __shared__ __attribute__((aligned(16))) uint2 smem[];
+  const int n = 1 << logn, k = 1 << logk, G = 1 << logG;
+  const uint64_t npos = slen / 2;
+  const uint64_t pos0 = uint64_t(blockIdx.x) * 4 * G;
+  const uint8_t *SH = shards + uint64_t(blockIdx.y) * nv * sstride;
+  const uint8_t *pr = present + uint64_t(blockIdx.y) * n;
+  const uint16_t *E = elog + uint64_t(blockIdx.y) * n;
+  uint8_t *O = out + uint64_t(blockIdx.y) * ostride;
+  uint2 *S = smem, *D = smem + size_t(n) * G;
+  if (scratch) {
+    S = scratch + (uint64_t(blockIdx.y) * gridDim.x + blockIdx.x) * 2 * uint64_t(n) * G;
+    D = S + size_t(n) * G;
+  }
+  // gather the column, multiply present symbols by the locator (decode_main:174-177)
+  for (int e = threadIdx.x; e < n * G; e += blockDim.x) {
+    const int g = e & (G - 1), v = e >> logG;
+    uint32_t yl = 0, yh = 0;
+    if (v < nv && pr[v]) {
+      uint32_t xl = 0, xh = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t pos = pos0 + 4 * g + q;
+        if (pos < npos) {
+          xh |= uint32_t(SH[uint64_t(v) * sstride + 2 * pos]) << (8 * q);
+          xl |= uint32_t(SH[uint64_t(v) * sstride + 2 * pos + 1]) << (8 * q);
+        }
+      }
+      Tab T;
+      load_tab(t.mtab, mul_index(E[v]), T);
+      mul_acc(xl, xh, T, yl, yh);
+    }
+    S[e] = make_uint2(yl, yh);
+  }
+  __syncthreads();
+  ifft_g(S, logG, logn, 0, t);
+  // formal derivative (poly_encoder.hpp:195-215), closed form:
+  //   c'[j] = c[j] ^ XOR_{b : bit b of j is 0} c[j | 2^b]
+  for (int e = threadIdx.x; e < n * G; e += blockDim.x) {
+    const int g = e & (G - 1), j = e >> logG;
+    uint2 acc = S[e];
+    for (int b = 0; b < logn; ++b)
+      if (!(j & (1 << b))) {
+        const uint2 o = S[(j | (1 << b)) * G + g];
+        acc.x ^= o.x;
+        acc.y ^= o.y;
+      }
+    D[e] = acc;
+  }
+  __syncthreads();
+  fft_g(D, logG, logn, 0, t);
+  // erased systematic positions: * locator (decode_main:185-188); present: as received
+  for (int e = threadIdx.x; e < k * G; e += blockDim.x) {
+    const int g = e & (G - 1), y = e >> logG;
+    const bool have = y < nv && pr[y];
+    uint32_t xl = 0, xh = 0;
+    if (have) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t pos = pos0 + 4 * g + q;
+        if (pos < npos) {
+          xh |= uint32_t(SH[uint64_t(y) * sstride + 2 * pos]) << (8 * q);
+          xl |= uint32_t(SH[uint64_t(y) * sstride + 2 * pos + 1]) << (8 * q);
+        }
+      }
+    } else {
+      Tab T;
+      load_tab(t.mtab, mul_index(E[y]), T);
+      const uint2 r = D[e];
+      mul_acc(r.x, r.y, T, xl, xh);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint64_t pos = pos0 + 4 * g + q;
+      if (pos < npos) {
+        O[(pos * k + y) * 2] = uint8_t(xh >> (8 * q));
+        O[(pos * k + y) * 2 + 1] = uint8_t(xl >> (8 * q));
+      }
+    }
+  }
+}
+
+// reed-solomon.hpp:143-179: out[2(i*k + y) ..] = shard_y[2i ..]
+__global__ void __launch_bounds__(kBlock) systematic_g(const uint8_t *__restrict__ shards,
+                                                       uint64_t slen, uint64_t sstride, int nv,
+                                                       int logk, uint8_t *__restrict__ out,
+                                                       uint64_t ostride) {
+  const int k = 1 << logk;
+  const uint64_t npos = slen / 2;
+  const uint8_t *SH = shards + uint64_t(blockIdx.y) * nv * sstride;
+  uint8_t *O = out + uint64_t(blockIdx.y) * ostride;
+  const uint64_t total = npos * k;
+  for (uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < total;
+       e += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t i = e >> logk;
+    const int y = int(e & (k - 1));
+    O[2 * e] = SH[uint64_t(y) * sstride + 2 * i];
+    O[2 * e + 1] = SH[uint64_t(y) * sstride + 2 * i + 1];
+  }
+}
+
+int ilog2(uint32_t v) { return 31 - __builtin_clz(v); }
+
+int groups_for(uint32_t size) {  // byte-planar groups per workgroup
+  if (size >= kLdsSlots) return 1;
+  uint32_t g = kLdsSlots / size;
+  return int(g > 64 ? 64 : g);
+}
+
+}  // namespace
+
+size_t encode_scratch_bytes(const CodeParams &p, size_t plen, size_t batch) {
+  if (p.k <= uint32_t(kLdsSlots)) return 0;
+  const size_t pieces = shard_len(p.k, plen) / 2;
+  const size_t tiles = (pieces + 3) / 4;
+  return tiles * batch * 2 * size_t(p.k) * sizeof(uint2);
+}
+
+hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
+                         size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
+                         size_t sstride, void *scratch, hipStream_t s) {
+  if (batch == 0 || plen == 0) return hipSuccess;
+  const size_t sl = shard_len(p.k, plen);
+  const int G = groups_for(p.k);
+  const size_t tiles = (sl / 2 + 4 * G - 1) / (4 * G);
+  const bool lds = p.k <= uint32_t(kLdsSlots);
+  const size_t shm = lds ? 2 * size_t(p.k) * G * sizeof(uint2) : 0;
+  dim3 grid((unsigned)tiles, (unsigned)batch);
+  hipLaunchKernelGGL(encode_g, grid, dim3(kBlock), shm, s, d_payloads, uint64_t(plen),
+                     uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride), int(p.nv),
+                     ilog2(p.n), ilog2(p.k), ilog2(uint32_t(G)), t,
+                     lds ? nullptr : static_cast<uint2 *>(scratch));
+  return hipGetLastError();
+}
+
+size_t error_locator_scratch_bytes(const CodeParams &p, size_t batch) {
+  return p.n > 65536u ? batch * p.n * 2 : 0;
+}
+
+hipError_t launch_error_locator(const CodeParams &p, const uint8_t *d_present, size_t batch,
+                                const uint16_t *d_fold, uint16_t *d_err_log, void *scratch,
+                                hipStream_t s) {
+  if (batch == 0) return hipSuccess;
+  const size_t shm = size_t(p.n) * sizeof(uint16_t);
+  if (shm > 65536) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&error_locator_g),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, int(shm));
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(error_locator_g, dim3(unsigned(batch)), dim3(kBlock), shm, s, d_present,
+                     int(p.nv), ilog2(p.n), d_fold, d_err_log, static_cast<uint16_t *>(nullptr));
+  (void)scratch;
+  return hipGetLastError();
+}
+
+size_t reconstruct_scratch_bytes(const CodeParams &p, size_t slen, size_t batch) {
+  if (p.n <= uint32_t(kLdsSlots)) return 0;
+  const size_t tiles = (slen / 2 + 3) / 4;
+  return tiles * batch * 2 * size_t(p.n) * sizeof(uint2);
+}
+
+hipError_t launch_reconstruct(const CodeParams &p, const DevTables &t, const uint8_t *d_shards,
+                              size_t slen, size_t sstride, const uint8_t *d_present,
+                              const uint16_t *d_err_log, size_t batch, uint8_t *d_out,
+                              size_t ostride, void *scratch, hipStream_t s) {
+  if (batch == 0 || slen < 2) return hipSuccess;
+  const int G = groups_for(p.n);
+  const size_t tiles = (slen / 2 + 4 * G - 1) / (4 * G);
+  const bool lds = p.n <= uint32_t(kLdsSlots);
+  const size_t shm = lds ? 2 * size_t(p.n) * G * sizeof(uint2) : 0;
+  dim3 grid((unsigned)tiles, (unsigned)batch);
+  hipLaunchKernelGGL(reconstruct_g, grid, dim3(kBlock), shm, s, d_shards, uint64_t(slen),
+                     uint64_t(sstride), d_present, d_err_log, d_out, uint64_t(ostride), int(p.nv),
+                     ilog2(p.n), ilog2(p.k), ilog2(uint32_t(G)), t,
+                     lds ? nullptr : static_cast<uint2 *>(scratch));
+  return hipGetLastError();
+}
+
+hipError_t launch_systematic(const CodeParams &p, const uint8_t *d_shards, size_t slen,
+                             size_t sstride, size_t batch, uint8_t *d_out, size_t ostride,
+                             hipStream_t s) {
+  if (batch == 0 || slen < 2) return hipSuccess;
+  const size_t total = slen / 2 * p.k;
+  size_t blocks = (total + kBlock - 1) / kBlock;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(systematic_g, dim3(unsigned(blocks), unsigned(batch)), dim3(kBlock), 0, s,
+                     d_shards, uint64_t(slen), uint64_t(sstride), int(p.nv), ilog2(p.k), d_out,
+                     uint64_t(ostride));
+  return hipGetLastError();
+}
+
+}  // namespace ecamd

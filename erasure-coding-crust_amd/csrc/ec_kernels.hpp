@@ -1,0 +1,41 @@
+// ec_kernels.hpp — launch interface of the HIP kernels (internal, C++).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "gf_field.hpp"
+
+namespace ecamd {
+
+struct DevTables {
+  const uint16_t *skews = nullptr;  // 65535
+  const MulTab *mtab = nullptr;     // 65536
+};
+
+// Scratch (global memory) needed by each launch for FFT sizes whose working
+// set does not fit LDS; 0 for the common sizes.
+size_t encode_scratch_bytes(const CodeParams &p, size_t payload_len, size_t batch);
+size_t reconstruct_scratch_bytes(const CodeParams &p, size_t shard_len, size_t batch);
+
+hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
+                         size_t payload_len, size_t payload_stride, size_t batch, uint8_t *d_shards,
+                         size_t shard_stride, void *scratch, hipStream_t s);
+
+hipError_t launch_error_locator(const CodeParams &p, const uint8_t *d_present, size_t batch,
+                                const uint16_t *d_fold, uint16_t *d_err_log, void *scratch,
+                                hipStream_t s);
+size_t error_locator_scratch_bytes(const CodeParams &p, size_t batch);
+
+hipError_t launch_reconstruct(const CodeParams &p, const DevTables &t, const uint8_t *d_shards,
+                              size_t shard_len, size_t shard_stride, const uint8_t *d_present,
+                              const uint16_t *d_err_log, size_t batch, uint8_t *d_out,
+                              size_t out_stride, void *scratch, hipStream_t s);
+
+hipError_t launch_systematic(const CodeParams &p, const uint8_t *d_shards, size_t shard_len,
+                             size_t shard_stride, size_t batch, uint8_t *d_out, size_t out_stride,
+                             hipStream_t s);
+
+}  // namespace ecamd

@@ -1,0 +1,68 @@
+// gf_field.hpp — host-side GF(2^16) field description for the NPB codec.
+//
+// The field, its relabelled LOG/EXP tables and the additive-FFT skews are
+// defined by include/ec-cpp/f2e16.hpp:25-94 and additive_fft.hpp:45-97 of the
+// reference; this is an independent builder that produces the same values
+// (pinned by tests/test_capi_cpu.py against tests/golden/tables.json).
+//
+// The device never sees LOG/EXP: every multiply-by-constant runs through a
+// MulTab, a 20-dword v_perm lookup table per log-domain constant (see
+// ec_device.hpp for the byte-planar kernel arithmetic).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace ecamd {
+
+constexpr uint32_t kFieldSize = 65536;
+constexpr uint32_t kOneMask = 65535;
+
+// 80-byte multiply table for one constant c (log domain).  The 16-bit symbol
+// x = xH:xL is split into 3-bit groups xL[0:3) xL[3:6) xH[0:3) xH[3:6) and
+// 2-bit groups xL[6:8) xH[6:8); each group value indexes an 8- (or 4-) entry
+// byte table of the partial product's low (L) and high (H) byte.
+//   w[0..3]  : group xL[0:3)   {L.lo, L.hi, H.lo, H.hi}
+//   w[4..7]  : group xL[3:6)
+//   w[8..11] : group xH[0:3)
+//   w[12..15]: group xH[3:6)
+//   w[16..19]: {L(xL[6:8)), H(xL[6:8)), L(xH[6:8)), H(xH[6:8))}
+struct MulTab {
+  uint32_t w[20];
+};
+static_assert(sizeof(MulTab) == 80, "MulTab layout");
+
+// Index of the all-zero table: skews equal to 0xFFFF (log of the element 0)
+// mean "no multiply" in additive_fft.hpp:110,129 == multiply by zero.
+constexpr uint32_t kZeroTab = 65535;
+
+struct Field {
+  std::vector<uint16_t> log, exp, log_walsh;  // 65536 each (f2e16.hpp:48-84)
+  std::vector<uint16_t> skews;                // 65535 (additive_fft.hpp:47-97)
+  std::vector<MulTab> mtab;                   // 65536: [c] = *g^c, [65535] = *0
+
+  uint16_t mul(uint16_t x, uint32_t log_c) const {
+    if (x == 0) return 0;
+    uint32_t l = uint32_t(log[x]) + log_c;
+    return exp[(l & 0xffff) + (l >> 16)];
+  }
+  // F[lo] = sum_hi LOG_WALSH[hi*n + lo] mod 65535: folds the 65536-point
+  // error-locator transform onto n points (exactness: DESIGN.md §error locator).
+  std::vector<uint16_t> fold_log_walsh(uint32_t n) const;
+};
+
+const Field &field();  // built once, thread-safe
+
+// math.hpp:25-36, ec-cpp.cpp:15-37, reed-solomon.hpp:24-45,191-196
+struct CodeParams {
+  uint32_t nv = 0, n = 0, k = 0, threshold = 0;
+};
+enum class ParamError { kOk, kTooManyValidators, kNotEnoughValidators };
+ParamError code_params(unsigned long n_validators, CodeParams *out);
+inline size_t shard_len(uint32_t k, size_t payload_len) {
+  size_t syms = (payload_len + 1) / 2;
+  return (syms + k - 1) / k * 2;
+}
+
+}  // namespace ecamd

@@ -52,3 +52,35 @@ def present_mask(seed: int, n_validators: int, count: int, n: int | None = None)
     m = np.zeros(n if n is not None else n_validators, np.uint8)
     m[present_set(seed, n_validators, count)] = 1
     return m
+
+
+def present_masks(seeds, n_validators: int, count: int, n: int | None = None) -> np.ndarray:
+    """Vectorised erasure patterns for large batches (bench.py): for payload b keep
+    the ``count`` shards with the smallest splitmix64(seeds[b]) keys.  Seeded and
+    reproducible like ``present_set``; a different (faster) selection rule."""
+    seeds = list(seeds)
+    keys = np.stack([splitmix64_words(s, n_validators) for s in seeds])
+    order = np.argsort(keys, axis=1, kind="stable")[:, :count]
+    m = np.zeros((len(seeds), n if n is not None else n_validators), np.uint8)
+    np.put_along_axis(m, order, 1, axis=1)
+    return m
+
+
+def payloads_torch(seeds, length: int, device="cuda"):
+    """splitmix64 payloads generated on the device (bit-identical to ``payload``)."""
+    import torch
+
+    words = (length + 7) // 8
+    seed = torch.tensor([s & _M64 for s in seeds], dtype=torch.uint64).view(torch.int64)
+    seed = seed.to(device).view(-1, 1)
+    idx = torch.arange(1, words + 1, dtype=torch.int64, device=device).view(1, -1)
+
+    def lsr(x, s):
+        return (x >> s) & ((1 << (64 - s)) - 1)
+
+    g = _GOLDEN - (1 << 64)
+    z = seed + idx * g
+    z = (z ^ lsr(z, 30)) * (0xBF58476D1CE4E5B9 - (1 << 64))
+    z = (z ^ lsr(z, 27)) * (0x94D049BB133111EB - (1 << 64))
+    z = z ^ lsr(z, 31)
+    return z.view(torch.uint8).view(len(seeds), words * 8)[:, :length]

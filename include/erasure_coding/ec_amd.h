@@ -1,0 +1,80 @@
+/*
+ * ec_amd.h — MI355X device-resident batch extension of the erasure_coding.h
+ * C ABI.  These are NEW symbols (the nine ECCR_* entry points are unchanged).
+ *
+ * All pointers named d_* are device pointers on the codec's device; `stream`
+ * is a hipStream_t (NULL = the legacy default stream).  Calls are asynchronous
+ * on `stream` and capture-safe (no allocation, no synchronisation): the
+ * caller owns every buffer.  Results are bit-exact with ec-cpp:
+ *   encode      == ReedSolomon::encode      (include/ec-cpp/reed-solomon.hpp:47-81)
+ *   reconstruct == ReedSolomon::reconstruct (include/ec-cpp/reed-solomon.hpp:83-134)
+ *   systematic  == ReedSolomon::reconstruct_from_systematic (:143-179)
+ *
+ * Layouts (one batch = `batch` independent payloads of the same length):
+ *   payloads   : [batch][payload_stride] bytes, payload_len used
+ *   shards     : [batch][n_validators][shard_stride] bytes, shard_len used
+ *   present    : [batch][n] bytes, 1 = shard present (indices >= n_validators
+ *                are always treated as erased)
+ *   err_log    : [batch][n] uint16 log-domain erasure-locator multipliers
+ *                (poly_encoder.hpp:90-116), produced by ECCR_AMD_error_locator
+ *   out        : [batch][out_stride] bytes, shard_len * k used (zero-padded
+ *                past payload_len, as the reference)
+ */
+#ifndef ERASURE_CODING_EC_AMD_H_
+#define ERASURE_CODING_EC_AMD_H_
+
+#include "erasure_coding.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Code parameters for n_validators (ec-cpp.cpp:15-37): n = po2 >= nv,
+ * k = po2 <= threshold.  Host-only. */
+struct NPRSResult ECCR_AMD_code_params(unsigned long n_validators, unsigned long *n,
+                                       unsigned long *k, unsigned long *threshold);
+
+/* shard_len(payload_len) = ceil(ceil(len/2)/k)*2 (reed-solomon.hpp:191-196). */
+unsigned long ECCR_AMD_shard_len(unsigned long n_validators, unsigned long payload_len);
+
+/* Number of visible HIP devices (0 if none / runtime unusable). */
+int ECCR_AMD_device_count(void);
+
+/* Upload field tables and skews to the current device (idempotent). */
+struct NPRSResult ECCR_AMD_init_device(void);
+
+/* Device-resident batch encode. */
+struct NPRSResult ECCR_AMD_encode_batch(unsigned long n_validators, const uint8_t *d_payloads,
+                                        unsigned long payload_len, unsigned long payload_stride,
+                                        unsigned long batch, uint8_t *d_shards,
+                                        unsigned long shard_stride, void *stream);
+
+/* Erasure-locator multipliers for a batch of erasure patterns. */
+struct NPRSResult ECCR_AMD_error_locator(unsigned long n_validators, const uint8_t *d_present,
+                                         unsigned long batch, uint16_t *d_err_log,
+                                         void *stream);
+
+/* Device-resident batch reconstruct (needs ECCR_AMD_error_locator output).
+ * The caller guarantees >= k present shards per payload (the host C ABI
+ * checks this); missing shards' bytes are never read. */
+struct NPRSResult ECCR_AMD_reconstruct_batch(unsigned long n_validators, const uint8_t *d_shards,
+                                             unsigned long shard_len, unsigned long shard_stride,
+                                             const uint8_t *d_present, const uint16_t *d_err_log,
+                                             unsigned long batch, uint8_t *d_out,
+                                             unsigned long out_stride, void *stream);
+
+/* Device-resident batch reconstruct_from_systematic (shards 0..k-1 of each
+ * payload, same [batch][n_validators][shard_stride] layout). */
+struct NPRSResult ECCR_AMD_systematic_batch(unsigned long n_validators, const uint8_t *d_shards,
+                                            unsigned long shard_len, unsigned long shard_stride,
+                                            unsigned long batch, uint8_t *d_out,
+                                            unsigned long out_stride, void *stream);
+
+/* Last error message of the calling thread ("" if none). */
+const char *ECCR_AMD_last_error(void);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* ERASURE_CODING_EC_AMD_H_ */

@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU session: tests -> smoke -> bench -> rocprof.  Stops at the first
+# fault/abort/timeout (exit codes other than 0/1 from a test run).
+set -u
+OUT=${OUT:-gpurun_out}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -5 "$OUT/$name.log"
+  return $rc
+}
+ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+for s in "$@"; do
+  case $s in
+    test) step pytest_gpu 900 python -m pytest tests -m gpu -x -q; rc=$?; ok $rc || exit $rc ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; ok $rc || exit $rc ;;
+    bench_small) step bench_small 600 python bench.py --batch 512 --steps 3 --warmup 1 --cpu-seconds 3; rc=$?; ok $rc || exit $rc ;;
+    bench) step bench 900 python bench.py; rc=$?; ok $rc || exit $rc ;;
+    prof) step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --batch 1024 --steps 3 --warmup 1 --no-cpu-baseline; rc=$?; ok $rc || exit $rc ;;
+  esac
+done
