@@ -95,6 +95,7 @@ def main():
     n, k, thr = E.code_params(nv)
     cnt = {"threshold": thr, "k": k}.get(args.present) or int(args.present)
     sl = E.shard_len(nv, plen)
+    ss = (sl + 63) // 64 * 64  # device shard row stride (aligned rows)
     dev = torch.device("cuda", local)
 
     # synthetic inputs, resident before timing; seeds are global payload indices
@@ -103,7 +104,7 @@ def main():
     for c0 in range(0, B, 256):
         d_pay[c0:c0 + 256] = synth.payloads_torch(seeds[c0:c0 + 256], plen, device=dev)
     d_pres = torch.from_numpy(synth.present_masks([10**6 + s for s in seeds], nv, cnt, n)).to(dev)
-    d_sh = torch.empty((B, nv, sl), dtype=torch.uint8, device=dev)
+    d_sh = torch.empty((B, nv, ss), dtype=torch.uint8, device=dev)
     d_el = torch.empty((B, n), dtype=torch.int16, device=dev)
     d_out = torch.empty((B, sl * k), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -114,13 +115,13 @@ def main():
         if record:
             e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
             e[0].record(stream)
-        E.encode_batch(nv, d_pay, plen, plen, B, d_sh, sl, stream)
+        E.encode_batch(nv, d_pay, plen, plen, B, d_sh, ss, stream)
         if record:
             e[1].record(stream)
         E.error_locator(nv, d_pres, B, d_el, stream)
         if record:
             e[2].record(stream)
-        E.reconstruct_batch(nv, d_sh, sl, sl, d_pres, d_el, B, d_out, sl * k, stream)
+        E.reconstruct_batch(nv, d_sh, sl, ss, d_pres, d_el, B, d_out, sl * k, stream)
         if record:
             e[3].record(stream)
             ev.append(e)

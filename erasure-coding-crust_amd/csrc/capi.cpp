@@ -57,19 +57,21 @@ bool encode_host(const CodeParams &p, const uint8_t *payload, size_t len, HostCt
   DeviceState *d = device_state();
   if (!d) return false;
   const size_t sl = shard_len(p.k, len);
+  const size_t dstride = (sl + 15) / 16 * 16;  // aligned device rows for the fast kernels
   const size_t out_bytes = size_t(p.nv) * sl;
   if (!ensure_host(&c->h_in, &c->h_in_cap, len) ||
       !ensure_dev(reinterpret_cast<void **>(&c->d_in), &c->d_in_cap, len) ||
       !ensure_host(&c->h_out, &c->h_out_cap, out_bytes) ||
-      !ensure_dev(reinterpret_cast<void **>(&c->d_out), &c->d_out_cap, out_bytes))
+      !ensure_dev(reinterpret_cast<void **>(&c->d_out), &c->d_out_cap, size_t(p.nv) * dstride))
     return false;
   void *scratch = device_scratch(d, encode_scratch_bytes(p, len, 1));
   std::memcpy(c->h_in, payload, len);
   if (!hip_check(hipMemcpyAsync(c->d_in, c->h_in, len, hipMemcpyHostToDevice, c->stream), "H2D") ||
-      !hip_check(launch_encode(p, device_tables(d), c->d_in, len, len, 1, c->d_out, sl, scratch,
-                               c->stream),
+      !hip_check(launch_encode(p, device_tables(d), c->d_in, len, len, 1, c->d_out, dstride,
+                               scratch, c->stream),
                  "encode launch") ||
-      !hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost, c->stream),
+      !hip_check(hipMemcpy2DAsync(c->h_out, sl, c->d_out, dstride, sl, p.nv,
+                                  hipMemcpyDeviceToHost, c->stream),
                  "D2H") ||
       !hip_check(hipStreamSynchronize(c->stream), "encode"))
     return false;

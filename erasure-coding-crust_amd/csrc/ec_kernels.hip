@@ -306,6 +306,11 @@ hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t 
                          size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                          size_t sstride, void *scratch, hipStream_t s) {
   if (batch == 0 || plen == 0) return hipSuccess;
+  const bool aligned = (reinterpret_cast<uintptr_t>(d_payloads) % 16 == 0) &&
+                       (reinterpret_cast<uintptr_t>(d_shards) % 8 == 0) &&
+                       (batch == 1 || pstride % 16 == 0) && sstride % 8 == 0;
+  if (aligned && k256_applicable(p))
+    return launch_encode_k256(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
   const size_t sl = shard_len(p.k, plen);
   const int G = groups_for(p.k);
   const size_t tiles = (sl / 2 + 4 * G - 1) / (4 * G);

@@ -38,4 +38,10 @@ hipError_t launch_systematic(const CodeParams &p, const uint8_t *d_shards, size_
                              size_t shard_stride, size_t batch, uint8_t *d_out, size_t out_stride,
                              hipStream_t s);
 
+// specialised kernels (enc_k256.hip)
+bool k256_applicable(const CodeParams &p);
+hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
+                              size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
+                              size_t sstride, hipStream_t s);
+
 }  // namespace ecamd

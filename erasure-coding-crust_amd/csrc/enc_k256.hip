@@ -1,0 +1,357 @@
+// enc_k256.hip — encode kernel specialised for k = 256, n = 1024
+// (n_validators 766..1024, the BASELINE headline configuration).
+//
+// Work decomposition:
+//  * persistent: one 512-thread workgroup per CU, looping over tiles of 128
+//    consecutive pieces (piece = 512 payload bytes = 256 GF(2^16) symbols);
+//  * wave w owns pieces [16w, 16w+16) of the tile: 2 "instances" (lanes
+//    0-31 / 32-63) x 2 byte-planar groups (registers) x 4 pieces;
+//  * within an instance, lane q holds 8 of the 256 positions in registers:
+//    every radix-8 pass runs 3 butterfly stages in registers, then the wave
+//    re-distributes positions through its private LDS region;
+//  * multiplies: v_perm tables (ec_device.hpp) for every skew the k=256 /
+//    n=1024 code uses (1023 x 80 B) are resident in LDS for the whole kernel;
+//  * shard stores: results are staged in LDS as [shard row][128 pieces] and
+//    written as 256-byte contiguous row segments (two rows per wave store).
+// Butterflies, skew indices and the encodeLow structure follow
+// include/ec-cpp/additive_fft.hpp:99-141 and poly_encoder.hpp:217-240.
+#include <hip/hip_runtime.h>
+
+#include "ec_device.hpp"
+#include "ec_kernels.hpp"
+
+namespace ecamd {
+namespace {
+
+constexpr int K = 256;
+constexpr int N = 1024;
+constexpr int WAVES = 8;
+constexpr int THREADS = 64 * WAVES;
+constexpr int TILE = 16 * WAVES;  // pieces per tile
+constexpr int TAB_BYTES = 80;
+constexpr int TAB_REGION = 1024 * TAB_BYTES;  // skew idx 0..1022
+constexpr int XCH_BYTES = 256 * 32 + 32 * 32; // per-wave exchange region (padded)
+constexpr int LDS_BYTES = TAB_REGION + WAVES * XCH_BYTES;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+static_assert(256 * 256 <= WAVES * XCH_BYTES, "staging fits the exchange regions");
+
+struct State {
+  uint32_t l[2][8], h[2][8];  // [group][register]: low / high byte planes
+};
+
+__device__ __forceinline__ void lds_tab(const uint8_t *lds, uint32_t idx, Tab &T) {
+  const uint4 *p = reinterpret_cast<const uint4 *>(lds + idx * TAB_BYTES);
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const uint4 v = p[q];
+    T.t[4 * q] = v.x;
+    T.t[4 * q + 1] = v.y;
+    T.t[4 * q + 2] = v.z;
+    T.t[4 * q + 3] = v.w;
+  }
+}
+
+// skew index of the block holding position pos_a at stage m (additive_fft.hpp:108,126)
+__device__ __forceinline__ uint32_t skew_idx(uint32_t pos_a, int m, uint32_t offset) {
+  const uint32_t d = 1u << m;
+  return (pos_a & ~(2 * d - 1)) + d - 1 + offset;
+}
+
+__device__ __forceinline__ void ibfly(State &s, int ra, int rb, const Tab &T) {
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    s.l[g][rb] ^= s.l[g][ra];
+    s.h[g][rb] ^= s.h[g][ra];
+    mul_acc(s.l[g][rb], s.h[g][rb], T, s.l[g][ra], s.h[g][ra]);
+  }
+}
+
+__device__ __forceinline__ void fbfly(State &s, int ra, int rb, const Tab &T) {
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    mul_acc(s.l[g][rb], s.h[g][rb], T, s.l[g][ra], s.h[g][ra]);
+    s.l[g][rb] ^= s.l[g][ra];
+    s.h[g][rb] ^= s.h[g][ra];
+  }
+}
+
+// radix-8 pass over 3 consecutive position bits b0..b0+2 held in registers:
+// pos(r) = base | (r << b0).  Inverse: stages b0, b0+1, b0+2.
+__device__ __forceinline__ void ipass3(State &s, const uint8_t *tabs, uint32_t base, int b0,
+                                       uint32_t off) {
+  Tab T;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {  // stage b0: 4 distinct skews
+    lds_tab(tabs, skew_idx(base | (uint32_t(2 * rr) << b0), b0, off), T);
+    ibfly(s, 2 * rr, 2 * rr + 1, T);
+  }
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {  // stage b0+1: 2 distinct skews
+    lds_tab(tabs, skew_idx(base | (uint32_t(4 * hh) << b0), b0 + 1, off), T);
+    ibfly(s, 4 * hh, 4 * hh + 2, T);
+    ibfly(s, 4 * hh + 1, 4 * hh + 3, T);
+  }
+  lds_tab(tabs, skew_idx(base, b0 + 2, off), T);  // stage b0+2: 1 skew
+#pragma unroll
+  for (int r = 0; r < 4; ++r) ibfly(s, r, r + 4, T);
+}
+
+// forward: stages b0+2, b0+1, b0
+__device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t base, int b0,
+                                       uint32_t off) {
+  Tab T;
+  lds_tab(tabs, skew_idx(base, b0 + 2, off), T);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) fbfly(s, r, r + 4, T);
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    lds_tab(tabs, skew_idx(base | (uint32_t(4 * hh) << b0), b0 + 1, off), T);
+    fbfly(s, 4 * hh, 4 * hh + 2, T);
+    fbfly(s, 4 * hh + 1, 4 * hh + 3, T);
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    lds_tab(tabs, skew_idx(base | (uint32_t(2 * rr) << b0), b0, off), T);
+    fbfly(s, 2 * rr, 2 * rr + 1, T);
+  }
+}
+
+// layout C: register bit0 = p6, bit1 = p7, bit2 = p5 (passenger); stages 6, 7
+// have lane-uniform skews.
+__device__ __forceinline__ void ipassC(State &s, const uint8_t *tabs, uint32_t off) {
+  Tab T;
+#pragma unroll
+  for (int p7 = 0; p7 < 2; ++p7) {  // stage 6: skew depends on p7
+    lds_tab(tabs, skew_idx(uint32_t(p7) << 7, 6, off), T);
+    ibfly(s, 2 * p7, 2 * p7 + 1, T);
+    ibfly(s, 2 * p7 + 4, 2 * p7 + 5, T);
+  }
+  lds_tab(tabs, skew_idx(0, 7, off), T);  // stage 7
+  ibfly(s, 0, 2, T);
+  ibfly(s, 1, 3, T);
+  ibfly(s, 4, 6, T);
+  ibfly(s, 5, 7, T);
+}
+
+__device__ __forceinline__ void fpassC(State &s, const uint8_t *tabs, uint32_t off) {
+  Tab T;
+  lds_tab(tabs, skew_idx(0, 7, off), T);
+  fbfly(s, 0, 2, T);
+  fbfly(s, 1, 3, T);
+  fbfly(s, 4, 6, T);
+  fbfly(s, 5, 7, T);
+#pragma unroll
+  for (int p7 = 0; p7 < 2; ++p7) {
+    lds_tab(tabs, skew_idx(uint32_t(p7) << 7, 6, off), T);
+    fbfly(s, 2 * p7, 2 * p7 + 1, T);
+    fbfly(s, 2 * p7 + 4, 2 * p7 + 5, T);
+  }
+}
+
+// position held in register r by lane q (0..31) in each layout
+__device__ __forceinline__ uint32_t posA(uint32_t q, int r) { return (q << 3) | uint32_t(r); }
+__device__ __forceinline__ uint32_t posB(uint32_t q, int r) {
+  return ((q >> 3) << 6) | (uint32_t(r) << 3) | (q & 7);
+}
+__device__ __forceinline__ uint32_t posC(uint32_t q, int r) {
+  return (uint32_t(r & 3) << 6) | (uint32_t(r >> 2) << 5) | q;
+}
+
+// wave-private exchange: [pos][inst][group] uint2, rows padded every 8 positions
+__device__ __forceinline__ uint32_t xaddr(uint32_t pos, uint32_t inst) {
+  return pos * 32 + (pos >> 3) * 32 + inst * 16;
+}
+
+enum Layout { LA, LB, LC };
+
+template <Layout L>
+__device__ __forceinline__ uint32_t layout_pos(uint32_t q, int r) {
+  return L == LA ? posA(q, r) : (L == LB ? posB(q, r) : posC(q, r));
+}
+
+template <Layout FROM, Layout TO>
+__device__ __forceinline__ void exchange(State &s, uint8_t *xch, uint32_t q, uint32_t inst) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+    *reinterpret_cast<uint4 *>(xch + xaddr(layout_pos<FROM>(q, r), inst)) =
+        make_uint4(s.l[0][r], s.h[0][r], s.l[1][r], s.h[1][r]);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(xch + xaddr(layout_pos<TO>(q, r), inst));
+    s.l[0][r] = v.x;
+    s.h[0][r] = v.y;
+    s.l[1][r] = v.z;
+    s.h[1][r] = v.w;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// staging row v (shard offset), 128 pieces x 2 bytes, 16-byte slots XOR-swizzled
+__device__ __forceinline__ uint32_t saddr(uint32_t v, uint32_t slot) {
+  return v * 256 + ((slot ^ ((v >> 3) & 15)) << 4);
+}
+
+// byte-planar group (4 pieces) -> big-endian u16 x4 (pieces 0..3 in order)
+__device__ __forceinline__ uint2 to_be(uint32_t l, uint32_t h) {
+  return make_uint2(vperm(l, h, 0x05010400u), vperm(l, h, 0x07030602u));
+}
+
+// registers in layout A -> LDS staging rows 0..255 (shard = s0 + row)
+__device__ __forceinline__ void stage_rows(const State &s, uint8_t *stg, uint32_t q, uint32_t inst,
+                                           uint32_t wave) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const uint32_t v = posA(q, r);
+    const uint2 a = to_be(s.l[0][r], s.h[0][r]);
+    const uint2 b = to_be(s.l[1][r], s.h[1][r]);
+    *reinterpret_cast<uint4 *>(stg + saddr(v, 2 * wave + inst)) = make_uint4(a.x, a.y, b.x, b.y);
+  }
+}
+
+// all waves: LDS rows -> shards [s0, s0+256), 256-byte row segments
+__device__ __forceinline__ void store_rows(const uint8_t *stg, uint8_t *SH, uint64_t sstride,
+                                           uint32_t s0, int nv, uint64_t piece0, uint64_t npieces,
+                                           uint32_t wave, uint32_t lane) {
+  const uint32_t c = lane & 31;  // 4 pieces per lane
+  const uint64_t p = piece0 + 4 * c;
+#pragma unroll 4
+  for (int it = 0; it < 16; ++it) {
+    const uint32_t v = uint32_t(it) * 16 + wave * 2 + (lane >> 5);
+    const uint32_t slot = c >> 1;
+    const uint2 val =
+        *reinterpret_cast<const uint2 *>(stg + saddr(v, slot) + 8 * (c & 1));
+    const uint32_t shard = s0 + v;
+    if (int(shard) >= nv) continue;
+    uint8_t *dst = SH + uint64_t(shard) * sstride + 2 * p;
+    if (p + 4 <= npieces) {
+      *reinterpret_cast<uint2 *>(dst) = val;
+    } else if (p < npieces) {
+      const uint32_t w[2] = {val.x, val.y};
+      for (uint64_t e = 0; e < npieces - p; ++e)
+        *reinterpret_cast<uint16_t *>(dst + 2 * e) = uint16_t(w[e >> 1] >> (16 * (e & 1)));
+    }
+  }
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict__ payloads,
+                                                       uint64_t plen, uint64_t pstride,
+                                                       uint8_t *__restrict__ shards, uint64_t slen,
+                                                       uint64_t sstride, int nv, uint32_t batch,
+                                                       DevTables t) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t *tabs = lds;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t inst = lane >> 5, q = lane & 31;
+  uint8_t *xch = lds + TAB_REGION + wave * XCH_BYTES;
+  uint8_t *stg = lds + TAB_REGION;
+
+  // resident multiply tables for skew indices 0..1022 (all FFTs of k=256, n=1024)
+  for (uint32_t i = tid; i < 1023 * 5; i += THREADS) {
+    const uint32_t slot = i / 5, part = i % 5;
+    const uint4 v = reinterpret_cast<const uint4 *>(t.mtab + t.skews[slot])[part];
+    *reinterpret_cast<uint4 *>(tabs + slot * TAB_BYTES + part * 16) = v;
+  }
+  __syncthreads();
+
+  const uint64_t npieces = slen / 2;
+  const uint32_t tiles_pp = uint32_t((npieces + TILE - 1) / TILE);
+  const uint64_t total = uint64_t(tiles_pp) * batch;
+  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    const uint64_t b = tile / tiles_pp;
+    const uint64_t piece0 = (tile % tiles_pp) * TILE;
+    const uint8_t *P = payloads + b * pstride;
+    uint8_t *SH = shards + b * uint64_t(nv) * sstride;
+
+    // ---- load 8 pieces x 16 bytes (positions 8q..8q+7), zero past plen
+    State s;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      uint4 d[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t piece = piece0 + wave * 16 + inst * 8 + g * 4 + u;
+        const uint64_t off = piece * 2 * K + 16 * q;
+        if (off + 16 <= plen) {
+          d[u] = *reinterpret_cast<const uint4 *>(P + off);
+        } else {
+          uint32_t w[4] = {0, 0, 0, 0};
+          for (uint64_t e = off; e < plen && e < off + 16; ++e)
+            w[(e - off) >> 2] |= uint32_t(P[e]) << (8 * ((e - off) & 3));
+          d[u] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      }
+      // 4x4 byte transposes: dword j of each piece = (hi_{2j}, lo_{2j}, hi_{2j+1}, lo_{2j+1})
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t D0 = (&d[0].x)[j], D1 = (&d[1].x)[j], D2 = (&d[2].x)[j], D3 = (&d[3].x)[j];
+        const uint32_t t0 = vperm(D1, D0, 0x05010400u), t1 = vperm(D1, D0, 0x07030602u);
+        const uint32_t u0 = vperm(D3, D2, 0x05010400u), u1 = vperm(D3, D2, 0x07030602u);
+        s.h[g][2 * j] = vperm(u0, t0, 0x05040100u);
+        s.l[g][2 * j] = vperm(u0, t0, 0x07060302u);
+        s.h[g][2 * j + 1] = vperm(u1, t1, 0x05040100u);
+        s.l[g][2 * j + 1] = vperm(u1, t1, 0x07060302u);
+      }
+    }
+
+    // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)
+    __syncthreads();  // previous tile's staging reads are done
+    stage_rows(s, stg, q, inst, wave);
+    __syncthreads();
+    store_rows(stg, SH, sstride, 0, nv, piece0, npieces, wave, lane);
+    __syncthreads();
+
+    // ---- IFFT_256 (index 0): passes A (bits 0-2), B (3-5), C (6-7)
+    ipass3(s, tabs, posA(q, 0), 0, 0);
+    exchange<LA, LB>(s, xch, q, inst);
+    ipass3(s, tabs, posB(q, 0), 3, 0);
+    exchange<LB, LC>(s, xch, q, inst);
+    ipassC(s, tabs, 0);
+    const State coef = s;
+
+    // ---- FFT_256 at each coset shift (encodeLow, poly_encoder.hpp:229-237)
+    for (uint32_t sh = K; sh < uint32_t(N) && int(sh) < nv; sh += K) {
+      s = coef;
+      fpassC(s, tabs, sh);
+      exchange<LC, LB>(s, xch, q, inst);
+      fpass3(s, tabs, posB(q, 0), 3, sh);
+      exchange<LB, LA>(s, xch, q, inst);
+      fpass3(s, tabs, posA(q, 0), 0, sh);
+      __syncthreads();  // all waves done with their exchange regions
+      stage_rows(s, stg, q, inst, wave);
+      __syncthreads();
+      store_rows(stg, SH, sstride, sh, nv, piece0, npieces, wave, lane);
+      __syncthreads();
+    }
+  }
+}
+
+bool k256_applicable(const CodeParams &p) { return p.k == 256 && p.n == 1024; }
+
+hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
+                              size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
+                              size_t sstride, hipStream_t s) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&encode_k256),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e != hipSuccess) return e;
+  }
+  const size_t sl = shard_len(p.k, plen);
+  const size_t tiles = (sl / 2 + TILE - 1) / TILE * batch;
+  const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
+  hipLaunchKernelGGL(encode_k256, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
+                     uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride),
+                     int(p.nv), uint32_t(batch), t);
+  return hipGetLastError();
+}
+
+}  // namespace ecamd

@@ -126,29 +126,34 @@ def test_measure_performance():
 
 
 # ---------------------------------------------------------------- device batch API
-def _batch_case(nv, plen, batch, cnt_key="threshold", seed0=0):
+def _batch_case(nv, plen, batch, cnt_key="threshold", seed0=0, pad=0):
+    """pad=0: tight rows (generic kernels); pad>0: rows aligned to `pad` bytes (fast kernels)."""
     import torch
     n, k, thr = E.code_params(nv)
     sl = E.shard_len(nv, plen)
+    ss = (sl + pad - 1) // pad * pad if pad else sl
     pay = np.stack([synth.payload(seed0 + b, plen) for b in range(batch)])
     cnt = {"threshold": thr, "k": k}[cnt_key]
     pres = np.stack([synth.present_mask(10**6 + seed0 + b, nv, cnt, n) for b in range(batch)])
     d_pay = torch.from_numpy(pay).cuda()
-    d_sh = torch.zeros((batch, nv, sl), dtype=torch.uint8, device="cuda")
+    d_sh = torch.zeros((batch, nv, ss), dtype=torch.uint8, device="cuda")
     d_pr = torch.from_numpy(pres).cuda()
     d_el = torch.zeros((batch, n), dtype=torch.int16, device="cuda")
     d_out = torch.zeros((batch, sl * k), dtype=torch.uint8, device="cuda")
-    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, sl)
+    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
     E.error_locator(nv, d_pr, batch, d_el)
-    E.reconstruct_batch(nv, d_sh, sl, sl, d_pr, d_el, batch, d_out, sl * k)
+    E.reconstruct_batch(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k)
     torch.cuda.synchronize()
-    return pay, pres, d_sh.cpu().numpy(), d_el.cpu().numpy().view(np.uint16), d_out.cpu().numpy()
+    sh = d_sh.cpu().numpy()[:, :, :sl].copy()
+    return pay, pres, sh, d_el.cpu().numpy().view(np.uint16), d_out.cpu().numpy()
 
 
-@pytest.mark.parametrize("nv,plen,batch", [(6, 300, 5), (1024, 5000, 3), (1024, 70000, 2),
-                                           (4096, 3001, 2), (100, 1, 4)])
-def test_batch_vs_oracle(oracle, nv, plen, batch):
-    pay, pres, sh, el, out = _batch_case(nv, plen, batch)
+@pytest.mark.parametrize("nv,plen,batch,pad", [
+    (6, 300, 5, 0), (1024, 5000, 3, 0), (1024, 70000, 2, 0), (4096, 3001, 2, 0), (100, 1, 4, 0),
+    (1024, 5000, 3, 64), (1024, 70000, 2, 16), (1024, 1, 3, 16), (1024, 511, 2, 8),
+    (1024, 131073, 2, 64), (1000, 99999, 2, 64), (800, 12345, 3, 64), (4096, 3001, 2, 64)])
+def test_batch_vs_oracle(oracle, nv, plen, batch, pad):
+    pay, pres, sh, el, out = _batch_case(nv, plen, batch, pad=pad)
     n, k, _ = E.code_params(nv)
     for b in range(batch):
         ref = oracle.encode(nv, pay[b].tobytes())
@@ -163,7 +168,7 @@ def test_batch_vs_oracle(oracle, nv, plen, batch):
 def test_batch_config2_roundtrip():
     """BASELINE config 2 shape (n_validators=1024, 1 MB payloads, 342 random shards):
     size-independent round trip + batch-vs-single equality on a batch of 8."""
-    pay, pres, sh, el, out = _batch_case(1024, 1_000_000, 8, seed0=100)
+    pay, pres, sh, el, out = _batch_case(1024, 1_000_000, 8, seed0=100, pad=64)
     for b in range(8):
         assert out[b][:1_000_000].tobytes() == pay[b].tobytes()
         assert not out[b][1_000_000:].any()  # zero padding, as the reference
