@@ -85,7 +85,8 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
   DeviceState *d = device_state();
   if (!d) return false;
   const size_t in_bytes = size_t(p.nv) * sl, out_bytes = sl * p.k;
-  if (!ensure_dev(reinterpret_cast<void **>(&c->d_in), &c->d_in_cap, in_bytes) ||
+  const size_t dstride = (sl + 15) / 16 * 16;  // aligned device rows for the fast kernels
+  if (!ensure_dev(reinterpret_cast<void **>(&c->d_in), &c->d_in_cap, size_t(p.nv) * dstride) ||
       !ensure_dev(reinterpret_cast<void **>(&c->d_out), &c->d_out_cap, out_bytes) ||
       !ensure_host(&c->h_out, &c->h_out_cap, out_bytes) ||
       !ensure_dev(reinterpret_cast<void **>(&c->d_present), &c->d_present_cap, p.n) ||
@@ -93,12 +94,14 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
     return false;
   bool all_systematic = true;
   for (uint32_t y = 0; y < p.k; ++y) all_systematic &= present[y] != 0;
-  if (!hip_check(hipMemcpyAsync(c->d_in, c->h_in, in_bytes, hipMemcpyHostToDevice, c->stream),
+  (void)in_bytes;
+  if (!hip_check(hipMemcpy2DAsync(c->d_in, dstride, c->h_in, sl, sl, p.nv, hipMemcpyHostToDevice,
+                                  c->stream),
                  "H2D"))
     return false;
   if (all_systematic) {
     // every systematic shard is present: decode == interleave (exact)
-    if (!hip_check(launch_systematic(p, c->d_in, sl, sl, 1, c->d_out, out_bytes, c->stream),
+    if (!hip_check(launch_systematic(p, c->d_in, sl, dstride, 1, c->d_out, out_bytes, c->stream),
                    "systematic launch"))
       return false;
   } else {
@@ -110,7 +113,7 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
                    "H2D present") ||
         !hip_check(launch_error_locator(p, c->d_present, 1, fold, c->d_elog, nullptr, c->stream),
                    "error locator launch") ||
-        !hip_check(launch_reconstruct(p, device_tables(d), c->d_in, sl, sl, c->d_present,
+        !hip_check(launch_reconstruct(p, device_tables(d), c->d_in, sl, dstride, c->d_present,
                                       c->d_elog, 1, c->d_out, out_bytes, scratch, c->stream),
                    "reconstruct launch"))
       return false;

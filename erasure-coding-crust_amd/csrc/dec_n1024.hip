@@ -1,0 +1,468 @@
+// dec_n1024.hip — reconstruct kernel specialised for n = 1024, k = 256
+// (n_validators 683..1024; BASELINE configs 2 and 3).
+//
+// Per workgroup tile: 32 shard columns (= 32 codewords of 1024 symbols,
+// poly_encoder.hpp:164-189), 8 waves, one byte-planar group of 4 columns per
+// wave.  Phases:
+//  1. gather+scale: thread v loads 64 B of shard row v and multiplies by the
+//     locator E[v] (one v_perm table per row, reused for 8 groups), writing
+//     each group into that group's wave-private LDS region;
+//  2. IFFT_1024: radix-16 register passes A (bits 0-3), B (4-7) and a radix-4
+//     pass C (8-9) with the exchanges going through the wave's region;
+//  3. formal derivative in closed form, c'[j] = c[j] ^ XOR_{b: j_b=0} c[j|2^b],
+//     register bits in place, lane bits via DPP / permlane swaps;
+//  4. FFT_1024 restricted to the k outputs that are read: stage 9 keeps
+//     v < 512, stage 8 keeps v < 256, then stages 7..0 on 4 registers per lane
+//     with register<->lane bit swaps by DPP / permlane (no LDS);
+//  5. output: erased y < k scaled by E[y]; present y copied from the shard;
+//     each lane writes 8 contiguous bytes of a 512-byte output row.
+#include <hip/hip_runtime.h>
+
+#include "ec_device.hpp"
+#include "ec_kernels.hpp"
+
+namespace ecamd {
+namespace {
+
+constexpr int N = 1024;
+constexpr int K = 256;
+constexpr int WAVES = 8;
+constexpr int THREADS = 64 * WAVES;
+constexpr int COLS = 4 * WAVES;  // shard positions per tile
+constexpr int TAB_BYTES = 80;
+constexpr int TAB_REGION = 1024 * TAB_BYTES;
+constexpr int REG_BYTES = N * 8;  // one wave's group: 1024 x uint2
+constexpr int LDS_BYTES = TAB_REGION + WAVES * REG_BYTES;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+static_assert(K * TAB_BYTES <= WAVES * REG_BYTES, "output tables fit the regions");
+
+// region address of position v: 8-byte slots XOR-swizzled so that every
+// access pattern used below (positions varying in bits 4-8, 0-3+8, 0-4) is
+// bank-conflict free
+__device__ __forceinline__ uint32_t raddr(uint32_t v) {
+  const uint32_t f = (v & 31) ^ ((v >> 4) & 31);
+  return ((v >> 5) << 8) | (f << 3);
+}
+
+__device__ __forceinline__ void lds_tab(const uint8_t *base, uint32_t idx, Tab &T) {
+  const uint4 *p = reinterpret_cast<const uint4 *>(base + idx * TAB_BYTES);
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const uint4 v = p[q];
+    T.t[4 * q] = v.x;
+    T.t[4 * q + 1] = v.y;
+    T.t[4 * q + 2] = v.z;
+    T.t[4 * q + 3] = v.w;
+  }
+}
+
+__device__ __forceinline__ uint32_t skew_idx(uint32_t pos_a, int m) {
+  const uint32_t d = 1u << m;
+  return (pos_a & ~(2 * d - 1)) + d - 1;  // FFT index 0 (poly_encoder.hpp:180,183)
+}
+
+struct S16 {
+  uint32_t l[16], h[16];
+};
+
+__device__ __forceinline__ void ib(S16 &s, int a, int b, const Tab &T) {
+  s.l[b] ^= s.l[a];
+  s.h[b] ^= s.h[a];
+  mul_acc(s.l[b], s.h[b], T, s.l[a], s.h[a]);
+}
+
+// inverse radix-16 pass over position bits b0..b0+3: pos(r) = base | (r << b0)
+__device__ __forceinline__ void ipass4(S16 &s, const uint8_t *tabs, uint32_t base, int b0) {
+  Tab T;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int d = 1 << t;
+#pragma unroll
+    for (int blk = 0; blk < 16; blk += 2 * d) {  // one skew per block of 2d registers
+      lds_tab(tabs, skew_idx(base | (uint32_t(blk) << b0), b0 + t), T);
+#pragma unroll
+      for (int i = 0; i < d; ++i) ib(s, blk + i, blk + i + d, T);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t dpp_xor(uint32_t x, int ctrl_sel) {
+  switch (ctrl_sel) {  // partner lane = lane + 2^b (lanes whose bit b is 0)
+    case 0: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x101, 0xf, 0xf, true));
+    case 1: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x102, 0xf, 0xf, true));
+    case 2: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x104, 0xf, 0xf, true));
+    default: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x108, 0xf, 0xf, true));
+  }
+}
+
+// value of lane (lane + 2^b) for lanes whose bit b is 0 (others: don't care)
+__device__ __forceinline__ uint32_t from_upper(uint32_t x, int b) {
+  if (b < 4) return dpp_xor(x, b);
+  if (b == 4) {
+    auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return r[1];
+  }
+  auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return r[1];
+}
+
+// swap register bit (pair x: bit=0, y: bit=1) with lane bit b
+__device__ __forceinline__ void swap_bit(uint32_t &x, uint32_t &y, int b, bool hi) {
+  if (b == 4) {
+    auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+    return;
+  }
+  if (b == 5) {
+    auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+    return;
+  }
+  const uint32_t send = hi ? x : y;  // lane bit 1 sends x, lane bit 0 sends y
+  uint32_t recv;
+  switch (b) {
+    case 0: recv = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0xB1, 0xf, 0xf, true)); break;  // quad [1,0,3,2]
+    case 1: recv = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x4E, 0xf, 0xf, true)); break;  // quad [2,3,0,1]
+    case 2: {
+      const uint32_t up = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x104, 0xf, 0xf, true));
+      const uint32_t dn = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x114, 0xf, 0xf, true));
+      recv = hi ? dn : up;
+      break;
+    }
+    default: recv = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x128, 0xf, 0xf, true)); break;  // row_ror:8
+  }
+  if (hi) x = recv;
+  else y = recv;
+}
+
+__device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ? 0u : c; }
+
+}  // namespace
+
+__global__ void __launch_bounds__(THREADS) reconstruct_n1024(
+    const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
+    const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
+    uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t batch, DevTables t) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t *tabs = lds;
+  uint8_t *regions = lds + TAB_REGION;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint8_t *my = regions + wave * REG_BYTES;
+
+  for (uint32_t i = tid; i < 1023 * 5; i += THREADS) {
+    const uint32_t slot = i / 5, part = i % 5;
+    reinterpret_cast<uint4 *>(tabs + slot * TAB_BYTES)[part] =
+        reinterpret_cast<const uint4 *>(t.mtab + t.skews[slot])[part];
+  }
+  __syncthreads();
+
+  const uint64_t ncols = slen / 2;
+  const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);
+  const uint64_t total = uint64_t(tiles_pp) * batch;
+  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    const uint64_t b = tile / tiles_pp;
+    const uint64_t col0 = (tile % tiles_pp) * COLS;
+    const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
+    const uint8_t *pr = present + b * N;
+    const uint16_t *E = elog + b * N;
+    uint8_t *O = out + b * ostride;
+
+    // ---- phase 1: gather + scale rows v = tid, tid + 512 (decode_main:174-177)
+    __syncthreads();  // previous tile's readers of the regions are done
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const uint32_t v = tid + half * THREADS;
+      uint32_t l[8], h[8];
+#pragma unroll
+      for (int g = 0; g < 8; ++g) l[g] = h[g] = 0;
+      if (int(v) < nv && pr[v]) {
+        const uint8_t *row = SH + uint64_t(v) * sstride + 2 * col0;
+        uint32_t w[16];
+        const uint64_t avail = slen - 2 * col0;  // bytes of this row inside the tile
+        if (avail >= 64) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint4 d = reinterpret_cast<const uint4 *>(row)[q];
+            w[4 * q] = d.x;
+            w[4 * q + 1] = d.y;
+            w[4 * q + 2] = d.z;
+            w[4 * q + 3] = d.w;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) w[q] = 0;
+          for (uint64_t e = 0; e < avail; ++e) w[e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
+        }
+        Tab T;
+        load_tab(t.mtab, mul_index(E[v]), T);
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {  // columns 4g..4g+3: words (h0 l0 h1 l1)(h2 l2 h3 l3)
+          const uint32_t a = w[2 * g], c = w[2 * g + 1];
+          const uint32_t xh = vperm(c, a, 0x06040200u), xl = vperm(c, a, 0x07050301u);
+          mul_acc(xl, xh, T, l[g], h[g]);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 8; ++g)
+        *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l[g], h[g]);
+    }
+    __syncthreads();
+
+    // ---- phase 2: IFFT_1024 on this wave's group
+    S16 s;
+    {  // layout A: v = 16*lane + r
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(16 * lane + r));
+        s.l[r] = x.x;
+        s.h[r] = x.y;
+      }
+      ipass4(s, tabs, 16 * lane, 0);
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        *reinterpret_cast<uint2 *>(my + raddr(16 * lane + r)) = make_uint2(s.l[r], s.h[r]);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    const uint32_t baseB = (lane & 15) | ((lane >> 4) << 8);  // layout B: bits 4-7 in registers
+    {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(baseB | (r << 4)));
+        s.l[r] = x.x;
+        s.h[r] = x.y;
+      }
+      ipass4(s, tabs, baseB, 4);
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        *reinterpret_cast<uint2 *>(my + raddr(baseB | (r << 4))) = make_uint2(s.l[r], s.h[r]);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    // layout C: r bit0 = p8, bit1 = p9, bit2 = p6, bit3 = p7; lane = p0..p5
+    auto posC = [&](int r) {
+      return lane | (uint32_t((r >> 2) & 3) << 6) | (uint32_t(r & 3) << 8);
+    };
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(posC(r)));
+      s.l[r] = x.x;
+      s.h[r] = x.y;
+    }
+    {
+      Tab T;
+#pragma unroll
+      for (int p9 = 0; p9 < 2; ++p9) {  // stage 8: skew depends on p9 only
+        lds_tab(tabs, skew_idx(uint32_t(p9) << 9, 8), T);
+#pragma unroll
+        for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi + 2 * p9, 4 * hi + 2 * p9 + 1, T);
+      }
+      lds_tab(tabs, skew_idx(0, 9), T);  // stage 9
+#pragma unroll
+      for (int hi = 0; hi < 4; ++hi) {
+        ib(s, 4 * hi, 4 * hi + 2, T);
+        ib(s, 4 * hi + 1, 4 * hi + 3, T);
+      }
+    }
+
+    // ---- phase 3: formal derivative (poly_encoder.hpp:195-215), closed form
+    {
+      S16 d = s;
+      // register bits: r bit0 = p8, bit1 = p9, bit2 = p6, bit3 = p7
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (!(r & (1 << rb))) {
+            d.l[r] ^= s.l[r | (1 << rb)];
+            d.h[r] ^= s.h[r | (1 << rb)];
+          }
+      // lane bits 0..5 = p0..p5
+#pragma unroll
+      for (int lb = 0; lb < 6; ++lb) {
+        const uint32_t m = ((lane >> lb) & 1) ? 0u : 0xffffffffu;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          d.l[r] ^= from_upper(s.l[r], lb) & m;
+          d.h[r] ^= from_upper(s.h[r], lb) & m;
+        }
+      }
+      s = d;
+    }
+
+    // ---- phase 4: FFT_1024 restricted to outputs < 256 (afft, additive_fft.hpp:121-141)
+    uint32_t ql[4], qh[4];  // live registers: r with p8 = p9 = 0 -> q = (p6, p7)
+    {
+      Tab T;
+      lds_tab(tabs, skew_idx(0, 9), T);  // stage 9: keep v < 512 (a-side only)
+#pragma unroll
+      for (int hi = 0; hi < 4; ++hi) {
+        mul_acc(s.l[4 * hi + 2], s.h[4 * hi + 2], T, s.l[4 * hi], s.h[4 * hi]);
+        mul_acc(s.l[4 * hi + 3], s.h[4 * hi + 3], T, s.l[4 * hi + 1], s.h[4 * hi + 1]);
+      }
+      lds_tab(tabs, skew_idx(0, 8), T);  // stage 8: keep v < 256
+#pragma unroll
+      for (int hi = 0; hi < 4; ++hi) {
+        mul_acc(s.l[4 * hi + 1], s.h[4 * hi + 1], T, s.l[4 * hi], s.h[4 * hi]);
+        ql[hi] = s.l[4 * hi];
+        qh[hi] = s.h[4 * hi];
+      }
+    }
+    __syncthreads();  // every wave is done with its region: reuse them for E[y] tables
+    for (uint32_t i = tid; i < K * 5; i += THREADS) {
+      const uint32_t y = i / 5, part = i % 5;
+      reinterpret_cast<uint4 *>(regions + y * TAB_BYTES)[part] =
+          reinterpret_cast<const uint4 *>(t.mtab + mul_index(E[y]))[part];
+    }
+    {
+      // q bit0 = p6, bit1 = p7; lane bits = p0..p5.  Positions < 256 only.
+      auto fb = [&](int a, int bb, const Tab &T) {
+        mul_acc(ql[bb], qh[bb], T, ql[a], qh[a]);
+        ql[bb] ^= ql[a];
+        qh[bb] ^= qh[a];
+      };
+      Tab T;
+      lds_tab(tabs, skew_idx(0, 7), T);  // stage 7
+      fb(0, 2, T);
+      fb(1, 3, T);
+#pragma unroll
+      for (int p7 = 0; p7 < 2; ++p7) {  // stage 6
+        lds_tab(tabs, skew_idx(uint32_t(p7) << 7, 6), T);
+        fb(2 * p7, 2 * p7 + 1, T);
+      }
+      // q (p6, p7) <-> lane bits 4, 5 (p4, p5)
+      swap_bit(ql[0], ql[1], 4, false);
+      swap_bit(qh[0], qh[1], 4, false);
+      swap_bit(ql[2], ql[3], 4, false);
+      swap_bit(qh[2], qh[3], 4, false);
+      swap_bit(ql[0], ql[2], 5, false);
+      swap_bit(qh[0], qh[2], 5, false);
+      swap_bit(ql[1], ql[3], 5, false);
+      swap_bit(qh[1], qh[3], 5, false);
+      // now q = (p4, p5); lane bits 0-3 = p0..p3, 4 = p6, 5 = p7
+      const uint32_t hi67 = ((lane >> 4) & 3) << 6;
+      const uint32_t lo = lane & 15;
+      lds_tab(tabs, skew_idx(hi67 | lo, 5), T);  // stage 5
+      fb(0, 2, T);
+      fb(1, 3, T);
+#pragma unroll
+      for (int p5 = 0; p5 < 2; ++p5) {  // stage 4
+        lds_tab(tabs, skew_idx(hi67 | (uint32_t(p5) << 5) | lo, 4), T);
+        fb(2 * p5, 2 * p5 + 1, T);
+      }
+      // q (p4, p5) <-> lane bits 2, 3 (p2, p3)
+      const bool l2 = (lane >> 2) & 1, l3 = (lane >> 3) & 1;
+      swap_bit(ql[0], ql[1], 2, l2);
+      swap_bit(qh[0], qh[1], 2, l2);
+      swap_bit(ql[2], ql[3], 2, l2);
+      swap_bit(qh[2], qh[3], 2, l2);
+      swap_bit(ql[0], ql[2], 3, l3);
+      swap_bit(qh[0], qh[2], 3, l3);
+      swap_bit(ql[1], ql[3], 3, l3);
+      swap_bit(qh[1], qh[3], 3, l3);
+      // now q = (p2, p3); lane bits 0,1 = p0,p1; 2,3 = p4,p5; 4,5 = p6,p7
+      const uint32_t hi47 = (((lane >> 2) & 15) << 4);
+      const uint32_t lo01 = lane & 3;
+      lds_tab(tabs, skew_idx(hi47 | lo01, 3), T);  // stage 3
+      fb(0, 2, T);
+      fb(1, 3, T);
+#pragma unroll
+      for (int p3 = 0; p3 < 2; ++p3) {  // stage 2
+        lds_tab(tabs, skew_idx(hi47 | (uint32_t(p3) << 3) | lo01, 2), T);
+        fb(2 * p3, 2 * p3 + 1, T);
+      }
+      // q (p2, p3) <-> lane bits 0, 1 (p0, p1)
+      const bool l0 = lane & 1, l1 = (lane >> 1) & 1;
+      swap_bit(ql[0], ql[1], 0, l0);
+      swap_bit(qh[0], qh[1], 0, l0);
+      swap_bit(ql[2], ql[3], 0, l0);
+      swap_bit(qh[2], qh[3], 0, l0);
+      swap_bit(ql[0], ql[2], 1, l1);
+      swap_bit(qh[0], qh[2], 1, l1);
+      swap_bit(ql[1], ql[3], 1, l1);
+      swap_bit(qh[1], qh[3], 1, l1);
+      // now q = (p0, p1); lane = (p2 .. p7): y = 4 * lane + q
+      const uint32_t hi27 = lane << 2;
+      lds_tab(tabs, skew_idx(hi27, 1), T);  // stage 1
+      fb(0, 2, T);
+      fb(1, 3, T);
+#pragma unroll
+      for (int p1 = 0; p1 < 2; ++p1) {  // stage 0
+        lds_tab(tabs, skew_idx(hi27 | (uint32_t(p1) << 1), 0), T);
+        fb(2 * p1, 2 * p1 + 1, T);
+      }
+    }
+    __syncthreads();  // E[y] tables in place
+
+    // ---- phase 5: y = 4*lane + q; columns col0 + 4*wave + c (decode_main:185-188,
+    // reconstructSub:138-149)
+    {
+      const uint64_t cbase = col0 + 4 * wave;
+      uint32_t ol[4], oh[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t y = 4 * lane + q;
+        ol[q] = oh[q] = 0;
+        if (int(y) < nv && pr[y]) {
+          const uint8_t *row = SH + uint64_t(y) * sstride + 2 * cbase;
+          uint32_t a = 0, c = 0;
+          if (cbase + 4 <= ncols) {
+            const uint2 d = *reinterpret_cast<const uint2 *>(row);
+            a = d.x;
+            c = d.y;
+          } else {
+            for (uint64_t e = 0; e < 2 * (ncols > cbase ? ncols - cbase : 0); ++e) {
+              if (e < 4) a |= uint32_t(row[e]) << (8 * e);
+              else c |= uint32_t(row[e]) << (8 * (e - 4));
+            }
+          }
+          oh[q] = vperm(c, a, 0x06040200u);
+          ol[q] = vperm(c, a, 0x07050301u);
+        } else {
+          Tab T;
+          lds_tab(regions, y, T);
+          mul_acc(ql[q], qh[q], T, ol[q], oh[q]);
+        }
+      }
+      // column c of the group: 4 consecutive y -> 8 bytes BE
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint64_t col = cbase + c;
+        if (col >= ncols) break;
+        const uint32_t w0 = vperm(ol[0], oh[0], 0x0c0c0400u + 0x0101u * c) |
+                            (vperm(ol[1], oh[1], 0x0c0c0400u + 0x0101u * c) << 16);
+        const uint32_t w1 = vperm(ol[2], oh[2], 0x0c0c0400u + 0x0101u * c) |
+                            (vperm(ol[3], oh[3], 0x0c0c0400u + 0x0101u * c) << 16);
+        *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);
+      }
+    }
+  }
+}
+
+bool n1024_applicable(const CodeParams &p) { return p.n == 1024 && p.k == 256; }
+
+hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
+                                    const uint8_t *d_shards, size_t slen, size_t sstride,
+                                    const uint8_t *d_present, const uint16_t *d_err_log,
+                                    size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&reconstruct_n1024),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e != hipSuccess) return e;
+  }
+  const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
+  const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
+  hipLaunchKernelGGL(reconstruct_n1024, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
+                     uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out,
+                     uint64_t(ostride), int(p.nv), uint32_t(batch), t);
+  return hipGetLastError();
+}
+
+}  // namespace ecamd

@@ -355,6 +355,12 @@ hipError_t launch_reconstruct(const CodeParams &p, const DevTables &t, const uin
                               const uint16_t *d_err_log, size_t batch, uint8_t *d_out,
                               size_t ostride, void *scratch, hipStream_t s) {
   if (batch == 0 || slen < 2) return hipSuccess;
+  const bool aligned = (reinterpret_cast<uintptr_t>(d_shards) % 16 == 0) &&
+                       (reinterpret_cast<uintptr_t>(d_out) % 8 == 0) && sstride % 16 == 0 &&
+                       (batch == 1 || ostride % 8 == 0);
+  if (aligned && n1024_applicable(p))
+    return launch_reconstruct_n1024(p, t, d_shards, slen, sstride, d_present, d_err_log, batch,
+                                    d_out, ostride, s);
   const int G = groups_for(p.n);
   const size_t tiles = (slen / 2 + 4 * G - 1) / (4 * G);
   const bool lds = p.n <= uint32_t(kLdsSlots);

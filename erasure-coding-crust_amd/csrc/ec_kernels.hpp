@@ -44,4 +44,11 @@ hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uin
                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                               size_t sstride, hipStream_t s);
 
+// specialised kernels (dec_n1024.hip)
+bool n1024_applicable(const CodeParams &p);
+hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
+                                    const uint8_t *d_shards, size_t slen, size_t sstride,
+                                    const uint8_t *d_present, const uint16_t *d_err_log,
+                                    size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s);
+
 }  // namespace ecamd
