@@ -29,12 +29,13 @@ constexpr int K = 256;
 constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
 constexpr int COLS = 4 * WAVES;  // shard positions per tile
-constexpr int TAB_BYTES = 80;
-constexpr int TAB_REGION = 1024 * TAB_BYTES;
+using Tabs = LdsTabs<1024>;
+using OutTabs = LdsTabs<256>;
+constexpr int TAB_REGION = Tabs::kBytes;
 constexpr int REG_BYTES = N * 8;  // one wave's group: 1024 x uint2
 constexpr int LDS_BYTES = TAB_REGION + WAVES * REG_BYTES;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
-static_assert(K * TAB_BYTES <= WAVES * REG_BYTES, "output tables fit the regions");
+static_assert(OutTabs::kBytes <= WAVES * REG_BYTES, "output tables fit the regions");
 
 // region address of position v: 8-byte slots XOR-swizzled so that every
 // access pattern used below (positions varying in bits 4-8, 0-3+8, 0-4) is
@@ -45,15 +46,7 @@ __device__ __forceinline__ uint32_t raddr(uint32_t v) {
 }
 
 __device__ __forceinline__ void lds_tab(const uint8_t *base, uint32_t idx, Tab &T) {
-  const uint4 *p = reinterpret_cast<const uint4 *>(base + idx * TAB_BYTES);
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    const uint4 v = p[q];
-    T.t[4 * q] = v.x;
-    T.t[4 * q + 1] = v.y;
-    T.t[4 * q + 2] = v.z;
-    T.t[4 * q + 3] = v.w;
-  }
+  Tabs::load(base, idx, T);
 }
 
 __device__ __forceinline__ uint32_t skew_idx(uint32_t pos_a, int m) {
@@ -151,11 +144,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint8_t *my = regions + wave * REG_BYTES;
 
-  for (uint32_t i = tid; i < 1023 * 5; i += THREADS) {
-    const uint32_t slot = i / 5, part = i % 5;
-    reinterpret_cast<uint4 *>(tabs + slot * TAB_BYTES)[part] =
-        reinterpret_cast<const uint4 *>(t.mtab + t.skews[slot])[part];
-  }
+  Tabs::fill(tabs, t.mtab, 1023, [&](uint32_t i) { return uint32_t(t.skews[i]); }, tid, THREADS);
   __syncthreads();
 
   const uint64_t ncols = slen / 2;
@@ -311,11 +300,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       }
     }
     __syncthreads();  // every wave is done with its region: reuse them for E[y] tables
-    for (uint32_t i = tid; i < K * 5; i += THREADS) {
-      const uint32_t y = i / 5, part = i % 5;
-      reinterpret_cast<uint4 *>(regions + y * TAB_BYTES)[part] =
-          reinterpret_cast<const uint4 *>(t.mtab + mul_index(E[y]))[part];
-    }
+    OutTabs::fill(regions, t.mtab, K, [&](uint32_t y) { return mul_index(E[y]); }, tid, THREADS);
     {
       // q bit0 = p6, bit1 = p7; lane bits = p0..p5.  Positions < 256 only.
       auto fb = [&](int a, int bb, const Tab &T) {
@@ -422,7 +407,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
           ol[q] = vperm(c, a, 0x07050301u);
         } else {
           Tab T;
-          lds_tab(regions, y, T);
+          OutTabs::load(regions, y, T);
           mul_acc(ql[q], qh[q], T, ol[q], oh[q]);
         }
       }

@@ -61,4 +61,39 @@ __device__ __forceinline__ void mul_acc(uint32_t xl, uint32_t xh, const Tab &T, 
   yh = h;
 }
 
+// LDS-resident multiply tables: plane-major (5 planes of 16-byte chunks), the
+// 16-byte slot of entry idx XOR-swizzled by f(idx) = (idx ^ idx>>4 ^ idx>>8) & 15.
+// f is injective on every set of entries one ds_read_b128 lane group touches in
+// the kernels (index strides 1..16 over the group's lanes, or 64 / 256 over <=4
+// distinct entries), so per-lane table loads are bank-conflict free.
+template <int ENTRIES>
+struct LdsTabs {
+  static constexpr int kPlane = ENTRIES * 16;
+  static constexpr int kBytes = 5 * kPlane;
+  __device__ static __forceinline__ uint32_t addr(uint32_t idx, uint32_t plane) {
+    const uint32_t f = (idx ^ (idx >> 4) ^ (idx >> 8)) & 15;
+    return plane * kPlane + ((idx >> 4) << 8) + (f << 4);
+  }
+  __device__ static __forceinline__ void load(const uint8_t *base, uint32_t idx, Tab &T) {
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(base + addr(idx, q));
+      T.t[4 * q] = v.x;
+      T.t[4 * q + 1] = v.y;
+      T.t[4 * q + 2] = v.z;
+      T.t[4 * q + 3] = v.w;
+    }
+  }
+  // cooperative fill: entry i <- mtab[src(i)]
+  template <typename F>
+  __device__ static __forceinline__ void fill(uint8_t *base, const MulTab *mtab, int count,
+                                              F src, uint32_t tid, uint32_t nthreads) {
+    for (uint32_t i = tid; i < uint32_t(count) * 5; i += nthreads) {
+      const uint32_t e = i / 5, q = i % 5;
+      *reinterpret_cast<uint4 *>(base + addr(e, q)) =
+          reinterpret_cast<const uint4 *>(mtab + src(e))[q];
+    }
+  }
+};
+
 }  // namespace ecamd

@@ -28,9 +28,9 @@ constexpr int N = 1024;
 constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
 constexpr int TILE = 16 * WAVES;  // pieces per tile
-constexpr int TAB_BYTES = 80;
-constexpr int TAB_REGION = 1024 * TAB_BYTES;  // skew idx 0..1022
-constexpr int XCH_BYTES = 256 * 32 + 32 * 32; // per-wave exchange region (padded)
+using Tabs = LdsTabs<1024>;
+constexpr int TAB_REGION = Tabs::kBytes;  // skew idx 0..1022
+constexpr int XCH_BYTES = 256 * 32;       // per-wave exchange region
 constexpr int LDS_BYTES = TAB_REGION + WAVES * XCH_BYTES;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 static_assert(256 * 256 <= WAVES * XCH_BYTES, "staging fits the exchange regions");
@@ -40,15 +40,7 @@ struct State {
 };
 
 __device__ __forceinline__ void lds_tab(const uint8_t *lds, uint32_t idx, Tab &T) {
-  const uint4 *p = reinterpret_cast<const uint4 *>(lds + idx * TAB_BYTES);
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    const uint4 v = p[q];
-    T.t[4 * q] = v.x;
-    T.t[4 * q + 1] = v.y;
-    T.t[4 * q + 2] = v.z;
-    T.t[4 * q + 3] = v.w;
-  }
+  Tabs::load(lds, idx, T);
 }
 
 // skew index of the block holding position pos_a at stage m (additive_fft.hpp:108,126)
@@ -157,9 +149,13 @@ __device__ __forceinline__ uint32_t posC(uint32_t q, int r) {
   return (uint32_t(r & 3) << 6) | (uint32_t(r >> 2) << 5) | q;
 }
 
-// wave-private exchange: [pos][inst][group] uint2, rows padded every 8 positions
+// wave-private exchange: 16-byte cell (pos, inst) = both groups; 256-byte
+// windows of 8 positions with the cell XOR-swizzled by h(window) so the layout
+// A/B/C reads (and layout A writes) are bank-conflict free
 __device__ __forceinline__ uint32_t xaddr(uint32_t pos, uint32_t inst) {
-  return pos * 32 + (pos >> 3) * 32 + inst * 16;
+  const uint32_t w = pos >> 3;
+  const uint32_t h = (w & 15) ^ ((w >> 3) & 1);
+  return (w << 8) | ((((pos & 7) * 2 + inst) ^ h) << 4);
 }
 
 enum Layout { LA, LB, LC };
@@ -251,11 +247,7 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
   uint8_t *stg = lds + TAB_REGION;
 
   // resident multiply tables for skew indices 0..1022 (all FFTs of k=256, n=1024)
-  for (uint32_t i = tid; i < 1023 * 5; i += THREADS) {
-    const uint32_t slot = i / 5, part = i % 5;
-    const uint4 v = reinterpret_cast<const uint4 *>(t.mtab + t.skews[slot])[part];
-    *reinterpret_cast<uint4 *>(tabs + slot * TAB_BYTES + part * 16) = v;
-  }
+  Tabs::fill(tabs, t.mtab, 1023, [&](uint32_t i) { return uint32_t(t.skews[i]); }, tid, THREADS);
   __syncthreads();
 
   const uint64_t npieces = slen / 2;
