@@ -256,29 +256,28 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       }
     }
 
-    // ---- phase 3: formal derivative (poly_encoder.hpp:195-215), closed form
+    // ---- phase 3: formal derivative (poly_encoder.hpp:195-215), closed form,
+    // in place: register r only needs partners r | 2^b > r (still original when
+    // r is processed in increasing order) and other lanes' original register r
     {
-      S16 d = s;
-      // register bits: r bit0 = p8, bit1 = p9, bit2 = p6, bit3 = p7
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
+      for (int r = 0; r < 16; ++r) {
+        uint32_t al = 0, ah = 0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (!(r & (1 << rb))) {
-            d.l[r] ^= s.l[r | (1 << rb)];
-            d.h[r] ^= s.h[r | (1 << rb)];
-          }
-      // lane bits 0..5 = p0..p5
-#pragma unroll
-      for (int lb = 0; lb < 6; ++lb) {
-        const uint32_t m = ((lane >> lb) & 1) ? 0u : 0xffffffffu;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          d.l[r] ^= from_upper(s.l[r], lb) & m;
-          d.h[r] ^= from_upper(s.h[r], lb) & m;
+        for (int lb = 0; lb < 6; ++lb) {  // lane bits 0..5 = p0..p5
+          const uint32_t m = ((lane >> lb) & 1) ? 0u : 0xffffffffu;
+          al ^= from_upper(s.l[r], lb) & m;
+          ah ^= from_upper(s.h[r], lb) & m;
         }
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)  // r bit0 = p8, bit1 = p9, bit2 = p6, bit3 = p7
+          if (!(r & (1 << rb))) {
+            al ^= s.l[r | (1 << rb)];
+            ah ^= s.h[r | (1 << rb)];
+          }
+        s.l[r] ^= al;
+        s.h[r] ^= ah;
       }
-      s = d;
     }
 
     // ---- phase 4: FFT_1024 restricted to outputs < 256 (afft, additive_fft.hpp:121-141)

@@ -26,6 +26,17 @@ __device__ __forceinline__ uint32_t vperm(uint32_t hi, uint32_t lo, uint32_t sel
   return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations
+// (lgkmcnt) but NOT for outstanding global stores/loads, unlike __syncthreads()
+// whose fence drains vmcnt and would serialize the HBM write stream with the
+// next tile's compute.  The asm "memory" clobbers stop compiler reordering of
+// LDS accesses across the barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 struct Tab {
   uint32_t t[20];
 };

@@ -25,18 +25,22 @@ namespace {
 
 constexpr int K = 256;
 constexpr int N = 1024;
-constexpr int WAVES = 8;
+// GP byte-planar groups per lane (registers), WAVES per workgroup.  GP = 1 with
+// 16 waves gives 4 waves/SIMD (<= 128 VGPRs) for latency hiding; the tile is
+// 128 pieces either way.
+constexpr int GP = 1;
+constexpr int WAVES = 16 / GP;
 constexpr int THREADS = 64 * WAVES;
-constexpr int TILE = 16 * WAVES;  // pieces per tile
+constexpr int TILE = 8 * GP * WAVES;  // pieces per tile
 using Tabs = LdsTabs<1024>;
 constexpr int TAB_REGION = Tabs::kBytes;  // skew idx 0..1022
-constexpr int XCH_BYTES = 256 * 32;       // per-wave exchange region
+constexpr int XCH_BYTES = 256 * 16 * GP;   // per-wave exchange region
 constexpr int LDS_BYTES = TAB_REGION + WAVES * XCH_BYTES;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
-static_assert(256 * 256 <= WAVES * XCH_BYTES, "staging fits the exchange regions");
+static_assert(TILE == 128 && 256 * 256 <= WAVES * XCH_BYTES, "staging fits the exchange regions");
 
 struct State {
-  uint32_t l[2][8], h[2][8];  // [group][register]: low / high byte planes
+  uint32_t l[GP][8], h[GP][8];  // [group][register]: low / high byte planes
 };
 
 __device__ __forceinline__ void lds_tab(const uint8_t *lds, uint32_t idx, Tab &T) {
@@ -51,7 +55,7 @@ __device__ __forceinline__ uint32_t skew_idx(uint32_t pos_a, int m, uint32_t off
 
 __device__ __forceinline__ void ibfly(State &s, int ra, int rb, const Tab &T) {
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < GP; ++g) {
     s.l[g][rb] ^= s.l[g][ra];
     s.h[g][rb] ^= s.h[g][ra];
     mul_acc(s.l[g][rb], s.h[g][rb], T, s.l[g][ra], s.h[g][ra]);
@@ -60,7 +64,7 @@ __device__ __forceinline__ void ibfly(State &s, int ra, int rb, const Tab &T) {
 
 __device__ __forceinline__ void fbfly(State &s, int ra, int rb, const Tab &T) {
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < GP; ++g) {
     mul_acc(s.l[g][rb], s.h[g][rb], T, s.l[g][ra], s.h[g][ra]);
     s.l[g][rb] ^= s.l[g][ra];
     s.h[g][rb] ^= s.h[g][ra];
@@ -149,45 +153,91 @@ __device__ __forceinline__ uint32_t posC(uint32_t q, int r) {
   return (uint32_t(r & 3) << 6) | (uint32_t(r >> 2) << 5) | q;
 }
 
-// wave-private exchange: 16-byte cell (pos, inst) = both groups; 256-byte
-// windows of 8 positions with the cell XOR-swizzled by h(window) so the layout
-// A/B/C reads (and layout A writes) are bank-conflict free
-__device__ __forceinline__ uint32_t xaddr(uint32_t pos, uint32_t inst) {
+// ---- wave-private exchange -------------------------------------------------
+// GP = 2: 16-byte cell (pos, inst) = both groups; 256-byte windows of 8 positions
+// with the cell XOR-swizzled by h(window) (layout A/B/C reads conflict-free).
+__device__ __forceinline__ uint32_t xaddr16(uint32_t pos, uint32_t inst) {
   const uint32_t w = pos >> 3;
   const uint32_t h = (w & 15) ^ ((w >> 3) & 1);
   return (w << 8) | ((((pos & 7) * 2 + inst) ^ h) << 4);
 }
+// GP = 1: 8-byte cell u = pos*2 + inst mapped by a GF(2)-linear bijection M
+// (found by search, scripts/search_swizzle.py) under which every layout's
+// reads (32-lane groups) and writes (16-lane groups) are bank-conflict free.
+// u = lane part XOR register part, so addr = M(lane part) ^ M(r part).
+constexpr uint32_t kM[9] = {0b110011100, 0b1001101, 0b111110100, 0b110001111, 0b11110011,
+                            0b101101010, 0b110000111, 0b111011000, 0b111100000};
+__host__ __device__ constexpr uint32_t mswz(uint32_t u) {
+  uint32_t a = 0;
+  for (int i = 0; i < 9; ++i) a |= uint32_t(__builtin_popcount(kM[i] & u) & 1) << i;
+  return a << 3;
+}
+// lane part / register part of u for each layout
+__device__ __forceinline__ uint32_t ulaneA(uint32_t q, uint32_t inst) { return (q << 4) | inst; }
+__device__ __forceinline__ uint32_t ulaneB(uint32_t q, uint32_t inst) {
+  return ((q >> 3) << 7) | ((q & 7) << 1) | inst;
+}
+__device__ __forceinline__ uint32_t ulaneC(uint32_t q, uint32_t inst) { return (q << 1) | inst; }
+__host__ __device__ constexpr uint32_t uregA(int r) { return uint32_t(r) << 1; }
+__host__ __device__ constexpr uint32_t uregB(int r) { return uint32_t(r) << 4; }
+__host__ __device__ constexpr uint32_t uregC(int r) {
+  return (uint32_t(r & 3) << 7) | (uint32_t(r >> 2) << 6);
+}
 
 enum Layout { LA, LB, LC };
 
+struct XBase {  // per-lane exchange base addresses (GP = 1)
+  uint32_t a, b, c;
+};
+
 template <Layout L>
-__device__ __forceinline__ uint32_t layout_pos(uint32_t q, int r) {
-  return L == LA ? posA(q, r) : (L == LB ? posB(q, r) : posC(q, r));
+__device__ __forceinline__ uint32_t xcell(const XBase &xb, uint32_t q, uint32_t inst, int r) {
+  if constexpr (GP == 1) {
+    if constexpr (L == LA) return xb.a ^ mswz(uregA(r));
+    else if constexpr (L == LB) return xb.b ^ mswz(uregB(r));
+    else return xb.c ^ mswz(uregC(r));
+  } else {
+    const uint32_t pos = L == LA ? posA(q, r) : (L == LB ? posB(q, r) : posC(q, r));
+    return xaddr16(pos, inst);
+  }
 }
 
 template <Layout FROM, Layout TO>
-__device__ __forceinline__ void exchange(State &s, uint8_t *xch, uint32_t q, uint32_t inst) {
+__device__ __forceinline__ void exchange(State &s, uint8_t *xch, const XBase &xb, uint32_t q,
+                                         uint32_t inst) {
 #pragma unroll
-  for (int r = 0; r < 8; ++r)
-    *reinterpret_cast<uint4 *>(xch + xaddr(layout_pos<FROM>(q, r), inst)) =
-        make_uint4(s.l[0][r], s.h[0][r], s.l[1][r], s.h[1][r]);
+  for (int r = 0; r < 8; ++r) {
+    if constexpr (GP == 1)
+      *reinterpret_cast<uint2 *>(xch + xcell<FROM>(xb, q, inst, r)) =
+          make_uint2(s.l[0][r], s.h[0][r]);
+    else
+      *reinterpret_cast<uint4 *>(xch + xcell<FROM>(xb, q, inst, r)) =
+          make_uint4(s.l[0][r], s.h[0][r], s.l[GP - 1][r], s.h[GP - 1][r]);
+  }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(xch + xaddr(layout_pos<TO>(q, r), inst));
-    s.l[0][r] = v.x;
-    s.h[0][r] = v.y;
-    s.l[1][r] = v.z;
-    s.h[1][r] = v.w;
+    if constexpr (GP == 1) {
+      const uint2 v = *reinterpret_cast<const uint2 *>(xch + xcell<TO>(xb, q, inst, r));
+      s.l[0][r] = v.x;
+      s.h[0][r] = v.y;
+    } else {
+      const uint4 v = *reinterpret_cast<const uint4 *>(xch + xcell<TO>(xb, q, inst, r));
+      s.l[0][r] = v.x;
+      s.h[0][r] = v.y;
+      s.l[GP - 1][r] = v.z;
+      s.h[GP - 1][r] = v.w;
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 
-// staging row v (shard offset), 128 pieces x 2 bytes, 16-byte slots XOR-swizzled
-__device__ __forceinline__ uint32_t saddr(uint32_t v, uint32_t slot) {
-  return v * 256 + ((slot ^ ((v >> 3) & 15)) << 4);
+// staging row v (shard offset), 128 pieces x 2 bytes; 8-byte slots XOR-swizzled
+// by the row's position block so the layout-A writes and row reads are conflict free
+__device__ __forceinline__ uint32_t saddr(uint32_t v, uint32_t slot8) {
+  return v * 256 + ((slot8 ^ ((v >> 3) & 31)) << 3);
 }
 
 // byte-planar group (4 pieces) -> big-endian u16 x4 (pieces 0..3 in order)
@@ -201,9 +251,10 @@ __device__ __forceinline__ void stage_rows(const State &s, uint8_t *stg, uint32_
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     const uint32_t v = posA(q, r);
-    const uint2 a = to_be(s.l[0][r], s.h[0][r]);
-    const uint2 b = to_be(s.l[1][r], s.h[1][r]);
-    *reinterpret_cast<uint4 *>(stg + saddr(v, 2 * wave + inst)) = make_uint4(a.x, a.y, b.x, b.y);
+#pragma unroll
+    for (int g = 0; g < GP; ++g)  // pieces 8P*wave + 4P*inst + 4g .. +3
+      *reinterpret_cast<uint2 *>(stg + saddr(v, (2 * GP * wave + GP * inst + g))) =
+          to_be(s.l[g][r], s.h[g][r]);
   }
 }
 
@@ -214,11 +265,9 @@ __device__ __forceinline__ void store_rows(const uint8_t *stg, uint8_t *SH, uint
   const uint32_t c = lane & 31;  // 4 pieces per lane
   const uint64_t p = piece0 + 4 * c;
 #pragma unroll 4
-  for (int it = 0; it < 16; ++it) {
-    const uint32_t v = uint32_t(it) * 16 + wave * 2 + (lane >> 5);
-    const uint32_t slot = c >> 1;
-    const uint2 val =
-        *reinterpret_cast<const uint2 *>(stg + saddr(v, slot) + 8 * (c & 1));
+  for (int it = 0; it < 128 / WAVES; ++it) {
+    const uint32_t v = uint32_t(it) * 2 * WAVES + wave * 2 + (lane >> 5);
+    const uint2 val = *reinterpret_cast<const uint2 *>(stg + saddr(v, c));
     const uint32_t shard = s0 + v;
     if (int(shard) >= nv) continue;
     uint8_t *dst = SH + uint64_t(shard) * sstride + 2 * p;
@@ -241,19 +290,30 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
                                                        DevTables t) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t inst = lane >> 5, q = lane & 31;
-  uint8_t *xch = lds + TAB_REGION + wave * XCH_BYTES;
+  const uint32_t tid0 = threadIdx.x;
   uint8_t *stg = lds + TAB_REGION;
 
   // resident multiply tables for skew indices 0..1022 (all FFTs of k=256, n=1024)
-  Tabs::fill(tabs, t.mtab, 1023, [&](uint32_t i) { return uint32_t(t.skews[i]); }, tid, THREADS);
+  Tabs::fill(tabs, t.mtab, 1023, [&](uint32_t i) { return uint32_t(t.skews[i]); }, tid0, THREADS);
   __syncthreads();
 
   const uint64_t npieces = slen / 2;
   const uint32_t tiles_pp = uint32_t((npieces + TILE - 1) / TILE);
   const uint64_t total = uint64_t(tiles_pp) * batch;
   for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    // lane ids made opaque per tile: per-lane LDS addresses are recomputed in the
+    // loop instead of being hoisted out of it and spilled
+    uint32_t tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const uint32_t lane = tid & 63, wave = tid >> 6;
+    const uint32_t inst = lane >> 5, q = lane & 31;
+    uint8_t *xch = lds + TAB_REGION + wave * XCH_BYTES;
+    XBase xb;
+    if constexpr (GP == 1) {
+      xb.a = mswz(ulaneA(q, inst));
+      xb.b = mswz(ulaneB(q, inst));
+      xb.c = mswz(ulaneC(q, inst));
+    }
     const uint64_t b = tile / tiles_pp;
     const uint64_t piece0 = (tile % tiles_pp) * TILE;
     const uint8_t *P = payloads + b * pstride;
@@ -262,11 +322,11 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     // ---- load 8 pieces x 16 bytes (positions 8q..8q+7), zero past plen
     State s;
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < GP; ++g) {
       uint4 d[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const uint64_t piece = piece0 + wave * 16 + inst * 8 + g * 4 + u;
+        const uint64_t piece = piece0 + wave * 8 * GP + inst * 4 * GP + g * 4 + u;
         const uint64_t off = piece * 2 * K + 16 * q;
         if (off + 16 <= plen) {
           d[u] = *reinterpret_cast<const uint4 *>(P + off);
@@ -291,33 +351,39 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     }
 
     // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)
-    __syncthreads();  // previous tile's staging reads are done
+    lds_barrier();  // previous tile's staging reads are done
     stage_rows(s, stg, q, inst, wave);
-    __syncthreads();
+    lds_barrier();
     store_rows(stg, SH, sstride, 0, nv, piece0, npieces, wave, lane);
-    __syncthreads();
+    lds_barrier();
 
     // ---- IFFT_256 (index 0): passes A (bits 0-2), B (3-5), C (6-7)
     ipass3(s, tabs, posA(q, 0), 0, 0);
-    exchange<LA, LB>(s, xch, q, inst);
+    exchange<LA, LB>(s, xch, xb, q, inst);
     ipass3(s, tabs, posB(q, 0), 3, 0);
-    exchange<LB, LC>(s, xch, q, inst);
+    exchange<LB, LC>(s, xch, xb, q, inst);
     ipassC(s, tabs, 0);
     const State coef = s;
 
     // ---- FFT_256 at each coset shift (encodeLow, poly_encoder.hpp:229-237)
     for (uint32_t sh = K; sh < uint32_t(N) && int(sh) < nv; sh += K) {
       s = coef;
+      // opaque copy: keeps the compiler from hoisting the first stage's selector
+      // masks out of the coset loop (that costs ~50 VGPRs and forces spills)
+#pragma unroll
+      for (int g = 0; g < GP; ++g)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(s.l[g][r]), "+v"(s.h[g][r]));
       fpassC(s, tabs, sh);
-      exchange<LC, LB>(s, xch, q, inst);
+      exchange<LC, LB>(s, xch, xb, q, inst);
       fpass3(s, tabs, posB(q, 0), 3, sh);
-      exchange<LB, LA>(s, xch, q, inst);
+      exchange<LB, LA>(s, xch, xb, q, inst);
       fpass3(s, tabs, posA(q, 0), 0, sh);
-      __syncthreads();  // all waves done with their exchange regions
+      lds_barrier();  // all waves done with their exchange regions
       stage_rows(s, stg, q, inst, wave);
-      __syncthreads();
+      lds_barrier();
       store_rows(stg, SH, sstride, sh, nv, piece0, npieces, wave, lane);
-      __syncthreads();
+      lds_barrier();
     }
   }
 }
