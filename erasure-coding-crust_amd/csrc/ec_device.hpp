@@ -7,7 +7,9 @@
 // over 3-bit (and 2-bit) bit groups of x.  Each T_g lookup of 4 symbols at
 // once is one v_perm_b32 (8-entry byte table held in two registers, selector
 // bytes = the 4 group values), i.e. 12 v_perm + 6 selector masks + 6 v_bitop3
-// per 4 multiply-accumulates.  No LOG/EXP gathers, no LDS bank conflicts.
+// per 4 multiply-accumulates.  No LOG/EXP gathers.  v_perm issues at half the
+// rate of v_and/v_bitop3 on gfx950 (scripts/micro/oprate.hip), so the perms are
+// ~60% of a multiply's issue slots and set the arithmetic ceiling.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -53,15 +55,28 @@ __device__ __forceinline__ void load_tab(const MulTab *__restrict__ mt, uint32_t
   }
 }
 
-// (yl, yh) ^= (xl, xh) * c, four symbols at once
+// {hi:lo} >> S as one v_lshrrev_b64: both byte planes' selector groups from one
+// (full-rate) instruction; the compiler narrows a C++ 64-bit shift back into
+// two 32-bit shifts, hence the asm (non-volatile: still scheduled and CSE'd).
+template <int S>
+__device__ __forceinline__ uint64_t shr64(uint64_t x) {
+  uint64_t r;
+  asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(S), "v"(x));
+  return r;
+}
+
+// (yl, yh) ^= (xl, xh) * c, four symbols at once: 12 v_perm (half rate on
+// gfx950), 6 v_and, 2 v_lshrrev_b64, 6 v_bitop3 = 38 issue slots.
 __device__ __forceinline__ void mul_acc(uint32_t xl, uint32_t xh, const Tab &T, uint32_t &yl,
                                         uint32_t &yh) {
+  const uint64_t x = (uint64_t(xh) << 32) | xl;
+  const uint64_t t3 = shr64<3>(x), t6 = shr64<6>(x);
   const uint32_t s0 = xl & 0x07070707u;
-  const uint32_t s1 = (xl >> 3) & 0x07070707u;
-  const uint32_t s2 = (xl >> 6) & 0x03030303u;
+  const uint32_t s1 = uint32_t(t3) & 0x07070707u;
+  const uint32_t s2 = uint32_t(t6) & 0x03030303u;
   const uint32_t s3 = xh & 0x07070707u;
-  const uint32_t s4 = (xh >> 3) & 0x07070707u;
-  const uint32_t s5 = (xh >> 6) & 0x03030303u;
+  const uint32_t s4 = uint32_t(t3 >> 32) & 0x07070707u;
+  const uint32_t s5 = uint32_t(t6 >> 32) & 0x03030303u;
   uint32_t l = xor3(yl, vperm(T.t[1], T.t[0], s0), vperm(T.t[5], T.t[4], s1));
   l = xor3(l, vperm(T.t[9], T.t[8], s3), vperm(T.t[13], T.t[12], s4));
   l = xor3(l, vperm(T.t[16], T.t[16], s2), vperm(T.t[18], T.t[18], s5));
