@@ -31,6 +31,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import ecc_amd as E  # noqa: E402
+import sharding  # noqa: E402
 import synth  # noqa: E402
 
 METRIC = "device-resident encode+reconstruct GiB/s (and % HBM roofline), n_val=1024"
@@ -99,7 +100,7 @@ def main():
     dev = torch.device("cuda", local)
 
     # synthetic inputs, resident before timing; seeds are global payload indices
-    seeds = [rank * B + b for b in range(B)]
+    seeds = sharding.rank_seeds(rank, B)
     d_pay = torch.empty((B, plen), dtype=torch.uint8, device=dev)
     for c0 in range(0, B, 256):
         d_pay[c0:c0 + 256] = synth.payloads_torch(seeds[c0:c0 + 256], plen, device=dev)
@@ -139,11 +140,7 @@ def main():
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
-    elapsed = t1 - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = sharding.max_over_ranks(t1 - t0, dist, dev)
 
     # sanity: the last step's reconstruction equals the payloads (round trip)
     ok = bool(torch.equal(d_out[:, :plen], d_pay))

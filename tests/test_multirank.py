@@ -1,0 +1,102 @@
+"""Multi-rank path on CPU (gloo, world_size 2): the payload sharding bench.py
+uses is disjoint and complete, ranks agree on the mixed-size partition without
+communicating, the max-over-ranks timing is the max, and encoding each rank's
+shard of payloads (oracle, CPU) gives exactly the single-process result —
+i.e. sharding by payload needs no data-path collective."""
+import hashlib
+import os
+import socket
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "erasure-coding-crust_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import sharding  # noqa: E402
+import synth  # noqa: E402
+
+NV, PLEN, PER_RANK = 16, 3001, 3
+MIXED = [15, 300, 5000, 100000, 1000, 7, 4096, 65536, 300, 15]
+
+
+def _digest(oracle, seeds):
+    h = hashlib.sha256()
+    for s in seeds:
+        for shard in oracle.encode(NV, synth.payload(s, PLEN).tobytes()):
+            h.update(shard)
+    return h.hexdigest()
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    import oracle as orc
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        seeds = sharding.rank_seeds(rank, PER_RANK)
+        all_seeds = [None] * world
+        dist.all_gather_object(all_seeds, seeds)
+        parts = sharding.balanced_partition(MIXED, world)
+        all_parts = [None] * world
+        dist.all_gather_object(all_parts, parts)
+        mx = sharding.max_over_ranks(10.0 + rank, dist)
+        digests = [None] * world
+        dist.all_gather_object(digests, _digest(orc.Oracle(), seeds))
+        if rank == 0:
+            q.put((all_seeds, all_parts, mx, digests))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_rank_sharding(oracle):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, port = 2, _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        all_seeds, all_parts, mx, digests = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    # weak-scaling ownership: disjoint, complete, independent of world size
+    flat = [s for r in all_seeds for s in r]
+    assert sorted(flat) == list(range(world * PER_RANK))
+    # every rank computed the same byte-balanced partition of the mixed stream
+    assert all(p == all_parts[0] for p in all_parts)
+    parts = all_parts[0]
+    assert sorted(i for p in parts for i in p) == list(range(len(MIXED)))
+    loads = [sum(MIXED[i] for i in p) for p in parts]
+    assert max(loads) - min(loads) <= max(MIXED)
+    assert mx == 11.0
+    # sharded encode == single-process encode of the same payloads
+    single = [_digest(oracle, sharding.rank_seeds(r, PER_RANK)) for r in range(world)]
+    assert digests == single
+
+
+@pytest.mark.parametrize("total,world", [(10, 3), (8, 8), (3, 4), (4096, 8)])
+def test_contiguous_range(total, world):
+    covered = []
+    for r in range(world):
+        s, c = sharding.contiguous_range(r, world, total)
+        covered += list(range(s, s + c))
+    assert covered == list(range(total))
+
+
+def test_balanced_partition_deterministic():
+    a = sharding.balanced_partition(MIXED, 4)
+    assert a == sharding.balanced_partition(list(MIXED), 4)
+    assert sorted(i for p in a for i in p) == list(range(len(MIXED)))
