@@ -20,6 +20,13 @@
 #include "ec_device.hpp"
 #include "ec_kernels.hpp"
 
+// ENC_ABL: ablation switches for scripts/micro/enc_ablate.cpp only (results are
+// wrong when set): 1 = no shard stores, 2 = one table load per pass,
+// 4 = no exchanges, 8 = no staging/stores at all.
+#ifndef ENC_ABL
+#define ENC_ABL 0
+#endif
+
 namespace ecamd {
 namespace {
 
@@ -43,7 +50,10 @@ struct State {
   uint32_t l[GP][8], h[GP][8];  // [group][register]: low / high byte planes
 };
 
-__device__ __forceinline__ void lds_tab(const uint8_t *lds, uint32_t idx, Tab &T) {
+__device__ __forceinline__ void lds_tab(const uint8_t *lds, uint32_t idx, Tab &T,
+                                        bool &first) {
+  if ((ENC_ABL & 2) && !first) return;
+  first = false;
   Tabs::load(lds, idx, T);
 }
 
@@ -76,18 +86,19 @@ __device__ __forceinline__ void fbfly(State &s, int ra, int rb, const Tab &T) {
 __device__ __forceinline__ void ipass3(State &s, const uint8_t *tabs, uint32_t base, int b0,
                                        uint32_t off) {
   Tab T;
+  bool first = true;
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {  // stage b0: 4 distinct skews
-    lds_tab(tabs, skew_idx(base | (uint32_t(2 * rr) << b0), b0, off), T);
+    lds_tab(tabs, skew_idx(base | (uint32_t(2 * rr) << b0), b0, off), T, first);
     ibfly(s, 2 * rr, 2 * rr + 1, T);
   }
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {  // stage b0+1: 2 distinct skews
-    lds_tab(tabs, skew_idx(base | (uint32_t(4 * hh) << b0), b0 + 1, off), T);
+    lds_tab(tabs, skew_idx(base | (uint32_t(4 * hh) << b0), b0 + 1, off), T, first);
     ibfly(s, 4 * hh, 4 * hh + 2, T);
     ibfly(s, 4 * hh + 1, 4 * hh + 3, T);
   }
-  lds_tab(tabs, skew_idx(base, b0 + 2, off), T);  // stage b0+2: 1 skew
+  lds_tab(tabs, skew_idx(base, b0 + 2, off), T, first);  // stage b0+2: 1 skew
 #pragma unroll
   for (int r = 0; r < 4; ++r) ibfly(s, r, r + 4, T);
 }
@@ -96,18 +107,19 @@ __device__ __forceinline__ void ipass3(State &s, const uint8_t *tabs, uint32_t b
 __device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t base, int b0,
                                        uint32_t off) {
   Tab T;
-  lds_tab(tabs, skew_idx(base, b0 + 2, off), T);
+  bool first = true;
+  lds_tab(tabs, skew_idx(base, b0 + 2, off), T, first);
 #pragma unroll
   for (int r = 0; r < 4; ++r) fbfly(s, r, r + 4, T);
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
-    lds_tab(tabs, skew_idx(base | (uint32_t(4 * hh) << b0), b0 + 1, off), T);
+    lds_tab(tabs, skew_idx(base | (uint32_t(4 * hh) << b0), b0 + 1, off), T, first);
     fbfly(s, 4 * hh, 4 * hh + 2, T);
     fbfly(s, 4 * hh + 1, 4 * hh + 3, T);
   }
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
-    lds_tab(tabs, skew_idx(base | (uint32_t(2 * rr) << b0), b0, off), T);
+    lds_tab(tabs, skew_idx(base | (uint32_t(2 * rr) << b0), b0, off), T, first);
     fbfly(s, 2 * rr, 2 * rr + 1, T);
   }
 }
@@ -116,13 +128,14 @@ __device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t b
 // have lane-uniform skews.
 __device__ __forceinline__ void ipassC(State &s, const uint8_t *tabs, uint32_t off) {
   Tab T;
+  bool first = true;
 #pragma unroll
   for (int p7 = 0; p7 < 2; ++p7) {  // stage 6: skew depends on p7
-    lds_tab(tabs, skew_idx(uint32_t(p7) << 7, 6, off), T);
+    lds_tab(tabs, skew_idx(uint32_t(p7) << 7, 6, off), T, first);
     ibfly(s, 2 * p7, 2 * p7 + 1, T);
     ibfly(s, 2 * p7 + 4, 2 * p7 + 5, T);
   }
-  lds_tab(tabs, skew_idx(0, 7, off), T);  // stage 7
+  lds_tab(tabs, skew_idx(0, 7, off), T, first);  // stage 7
   ibfly(s, 0, 2, T);
   ibfly(s, 1, 3, T);
   ibfly(s, 4, 6, T);
@@ -131,14 +144,15 @@ __device__ __forceinline__ void ipassC(State &s, const uint8_t *tabs, uint32_t o
 
 __device__ __forceinline__ void fpassC(State &s, const uint8_t *tabs, uint32_t off) {
   Tab T;
-  lds_tab(tabs, skew_idx(0, 7, off), T);
+  bool first = true;
+  lds_tab(tabs, skew_idx(0, 7, off), T, first);
   fbfly(s, 0, 2, T);
   fbfly(s, 1, 3, T);
   fbfly(s, 4, 6, T);
   fbfly(s, 5, 7, T);
 #pragma unroll
   for (int p7 = 0; p7 < 2; ++p7) {
-    lds_tab(tabs, skew_idx(uint32_t(p7) << 7, 6, off), T);
+    lds_tab(tabs, skew_idx(uint32_t(p7) << 7, 6, off), T, first);
     fbfly(s, 2 * p7, 2 * p7 + 1, T);
     fbfly(s, 2 * p7 + 4, 2 * p7 + 5, T);
   }
@@ -205,6 +219,7 @@ __device__ __forceinline__ uint32_t xcell(const XBase &xb, uint32_t q, uint32_t 
 template <Layout FROM, Layout TO>
 __device__ __forceinline__ void exchange(State &s, uint8_t *xch, const XBase &xb, uint32_t q,
                                          uint32_t inst) {
+  if (ENC_ABL & 4) return;
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     if constexpr (GP == 1)
@@ -248,6 +263,7 @@ __device__ __forceinline__ uint2 to_be(uint32_t l, uint32_t h) {
 // registers in layout A -> LDS staging rows 0..255 (shard = s0 + row)
 __device__ __forceinline__ void stage_rows(const State &s, uint8_t *stg, uint32_t q, uint32_t inst,
                                            uint32_t wave) {
+  if (ENC_ABL & 8) return;
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     const uint32_t v = posA(q, r);
@@ -262,6 +278,7 @@ __device__ __forceinline__ void stage_rows(const State &s, uint8_t *stg, uint32_
 __device__ __forceinline__ void store_rows(const uint8_t *stg, uint8_t *SH, uint64_t sstride,
                                            uint32_t s0, int nv, uint64_t piece0, uint64_t npieces,
                                            uint32_t wave, uint32_t lane) {
+  if (ENC_ABL & 9) return;
   const uint32_t c = lane & 31;  // 4 pieces per lane
   const uint64_t p = piece0 + 4 * c;
 #pragma unroll 4

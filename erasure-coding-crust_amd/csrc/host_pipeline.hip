@@ -1,0 +1,243 @@
+// host_pipeline.hip — host-resident batch encode / reconstruct (SURVEY.md
+// §8f row 2): the reference path starts and ends in host memory (block data
+// in, shards out), so these entry points stream a host batch through the GPU
+// in chunks, with three slots (stream + device buffers each) so that chunk
+// i's H2D, chunk i-1's kernels and chunk i-2's D2H overlap on the two copy
+// engines and the CUs.  Host buffers should be pinned (ECCR_AMD_host_alloc)
+// for full PCIe rate; pageable memory works but is staged by the runtime.
+//
+// Reconstruct takes only the present shards, compacted per payload
+// ([batch][cnt][sstride] + their indices), so PCIe carries exactly the bytes
+// the codec needs; `scatter_present` places them into codeword rows on the
+// device and builds the present mask for the error locator.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/erasure_coding/ec_amd.h"
+#include "ec_kernels.hpp"
+#include "ec_runtime.hpp"
+#include "gf_field.hpp"
+
+namespace ecamd {
+namespace {
+
+constexpr int kSlots = 3;
+
+// block (j, b): compact row j of payload b -> full row idx[b][j]; present[b][v] = 1
+__global__ void __launch_bounds__(256) scatter_present(const uint8_t *__restrict__ compact,
+                                                       uint64_t cstride, const uint16_t *__restrict__ idx,
+                                                       uint32_t cnt, uint64_t slen,
+                                                       uint8_t *__restrict__ full, uint64_t fstride,
+                                                       uint32_t nv, uint8_t *__restrict__ present,
+                                                       uint32_t n) {
+  const uint32_t b = blockIdx.y, j = blockIdx.x;
+  const uint32_t v = idx[uint64_t(b) * cnt + j];
+  if (v >= nv) return;  // validated on the host; never index out of the row block
+  const uint8_t *src = compact + (uint64_t(b) * cnt + j) * cstride;
+  uint8_t *dst = full + (uint64_t(b) * nv + v) * fstride;
+  if (threadIdx.x == 0) present[uint64_t(b) * n + v] = 1;
+  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  const uint64_t nvec = vec ? slen / 16 : 0;
+  for (uint64_t e = threadIdx.x; e < nvec; e += blockDim.x)
+    reinterpret_cast<uint4 *>(dst)[e] = reinterpret_cast<const uint4 *>(src)[e];
+  for (uint64_t e = nvec * 16 + threadIdx.x; e < slen; e += blockDim.x) dst[e] = src[e];
+}
+
+struct Slot {
+  hipStream_t stream = nullptr;
+  uint8_t *d_a = nullptr, *d_b = nullptr, *d_c = nullptr, *d_present = nullptr;
+  uint16_t *d_elog = nullptr, *d_idx = nullptr;
+  size_t cap_a = 0, cap_b = 0, cap_c = 0, cap_present = 0, cap_elog = 0, cap_idx = 0;
+};
+
+struct Pipeline {
+  Slot slot[kSlots];
+  int device = -1;
+};
+
+Pipeline *pipeline() {  // one per host thread (reentrant like the reference)
+  thread_local Pipeline pl;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (pl.device != dev) {
+    for (Slot &s : pl.slot) {
+      s = Slot{};
+      if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    }
+    pl.device = dev;
+  }
+  return &pl;
+}
+
+template <typename T>
+bool grow(T **p, size_t *cap, size_t bytes) {
+  return ensure_dev(reinterpret_cast<void **>(p), cap, bytes);
+}
+
+bool ok(hipError_t e, const char *what) {
+  if (e == hipSuccess) return true;
+  set_error(std::string("erasure_coding_crust(amd): ") + what + ": " + hipGetErrorString(e));
+  return false;
+}
+
+NPRSResult res(NPRSResult_Tag t) {
+  NPRSResult r;
+  std::memset(&r, 0, sizeof r);
+  r.tag = t;
+  return r;
+}
+
+size_t round16(size_t x) { return (x + 15) / 16 * 16; }
+
+}  // namespace
+}  // namespace ecamd
+
+using namespace ecamd;
+
+extern "C" {
+
+void *ECCR_AMD_host_alloc(unsigned long bytes) {
+  void *p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+
+void ECCR_AMD_host_free(void *p) {
+  if (p) (void)hipHostFree(p);
+}
+
+NPRSResult ECCR_AMD_encode_host_batch(unsigned long nv, const uint8_t *h_payloads,
+                                      unsigned long plen, unsigned long pstride,
+                                      unsigned long batch, uint8_t *h_shards,
+                                      unsigned long sstride, unsigned long chunk) {
+  CodeParams p;
+  if (code_params(nv, &p) != ParamError::kOk) return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+  if (plen == 0 || !h_payloads || !h_shards) return res(NPRS_RESULT_BAD_PAYLOAD);
+  const size_t sl = shard_len(p.k, plen);
+  if (pstride < plen || sstride < sl) return res(NPRS_RESULT_BAD_PAYLOAD);
+  DeviceState *d = device_state();
+  Pipeline *pl = d ? pipeline() : nullptr;
+  if (!pl) return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+  if (chunk == 0) chunk = 64;
+  // Device rows use the host stride (one linear copy) when it already suits the
+  // fast kernels or rows are short: a 2-D copy of many narrow rows is
+  // descriptor-bound (2-byte rows ran at ~10 us per row).  Otherwise rows are
+  // re-pitched to aligned device strides by a 2-D copy of long rows.
+  const bool pay_lin = pstride % 16 == 0 || plen < 256;
+  const bool sh_lin = sstride % 8 == 0 || sl < 256;
+  const size_t dps = pay_lin ? pstride : round16(plen);
+  const size_t dss = sh_lin ? sstride : (sl + 63) / 64 * 64;
+  for (unsigned long c0 = 0, i = 0; c0 < batch; c0 += chunk, ++i) {
+    Slot &s = pl->slot[i % kSlots];
+    const size_t cb = batch - c0 < chunk ? batch - c0 : chunk;
+    if (!grow(&s.d_a, &s.cap_a, chunk * dps) || !grow(&s.d_b, &s.cap_b, chunk * nv * dss))
+      return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+    void *scratch = device_scratch(d, encode_scratch_bytes(p, plen, cb));
+    const uint8_t *hp = h_payloads + c0 * pstride;
+    uint8_t *hs = h_shards + c0 * nv * sstride;
+    const hipError_t up =
+        pay_lin ? hipMemcpyAsync(s.d_a, hp, (cb - 1) * pstride + plen, hipMemcpyHostToDevice, s.stream)
+                : hipMemcpy2DAsync(s.d_a, dps, hp, pstride, plen, cb, hipMemcpyHostToDevice, s.stream);
+    if (!ok(up, "H2D payloads") ||
+        !ok(launch_encode(p, device_tables(d), s.d_a, plen, dps, cb, s.d_b, dss, scratch, s.stream),
+            "encode launch"))
+      return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+    const hipError_t down =
+        sh_lin ? hipMemcpyAsync(hs, s.d_b, (cb * nv - 1) * sstride + sl, hipMemcpyDeviceToHost,
+                                s.stream)
+               : hipMemcpy2DAsync(hs, sstride, s.d_b, dss, sl, cb * nv, hipMemcpyDeviceToHost,
+                                  s.stream);
+    if (!ok(down, "D2H shards"))
+      return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+  }
+  for (Slot &s : pl->slot)
+    if (!ok(hipStreamSynchronize(s.stream), "encode_host_batch"))
+      return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+  return res(NPRS_RESULT_OK);
+}
+
+NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_shards,
+                                           unsigned long slen, unsigned long sstride,
+                                           const uint16_t *h_index, unsigned long cnt,
+                                           unsigned long batch, uint8_t *h_out,
+                                           unsigned long ostride, unsigned long chunk) {
+  CodeParams p;
+  if (code_params(nv, &p) != ParamError::kOk) return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
+  if (!h_shards || !h_index || !h_out) return res(NPRS_RESULT_BAD_PAYLOAD);
+  if (slen % 2 != 0) return res(NPRS_RESULT_UNEVEN_LENGTH);
+  if (sstride < slen || ostride < slen * p.k) return res(NPRS_RESULT_NON_UNIFORM_CHUNKS);
+  if (cnt < p.k) return res(NPRS_RESULT_NOT_ENOUGH_CHUNKS);  // reed-solomon.hpp:99-100
+  // src/erasure_coding.rs:370-375 (index bounds) and reed-solomon.hpp:99-100
+  // (enough distinct shards; a repeated index counts once, its rows must agree)
+  std::vector<uint32_t> seen(nv, 0);
+  for (unsigned long b = 0; b < batch; ++b) {
+    unsigned long distinct = 0;
+    for (unsigned long j = 0; j < cnt; ++j) {
+      const uint16_t v = h_index[b * cnt + j];
+      if (v >= nv) {
+        NPRSResult r = res(NPRS_RESULT_CHUNK_INDEX_OUT_OF_BOUNDS);
+        r.chunk_index_out_of_bounds.chunk_index = v;
+        r.chunk_index_out_of_bounds.n_validators = nv;
+        return r;
+      }
+      if (seen[v] != b + 1) {
+        seen[v] = uint32_t(b + 1);
+        ++distinct;
+      }
+    }
+    if (distinct < p.k) return res(NPRS_RESULT_NOT_ENOUGH_CHUNKS);
+  }
+  DeviceState *d = device_state();
+  const uint16_t *fold = d ? device_fold(d, p.n) : nullptr;
+  Pipeline *pl = fold ? pipeline() : nullptr;
+  if (!pl) return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  if (chunk == 0) chunk = 64;
+  const size_t dss = (slen + 63) / 64 * 64, ob = slen * p.k;
+  const bool out_lin = ostride % 8 == 0 || ob < 256;  // as in encode: linear copy if it suits
+  const size_t dos = out_lin ? ostride : ob;
+  for (unsigned long c0 = 0, i = 0; c0 < batch; c0 += chunk, ++i) {
+    Slot &s = pl->slot[i % kSlots];
+    const size_t cb = batch - c0 < chunk ? batch - c0 : chunk;
+    if (!grow(&s.d_a, &s.cap_a, chunk * cnt * sstride) || !grow(&s.d_b, &s.cap_b, chunk * nv * dss) ||
+        !grow(&s.d_c, &s.cap_c, chunk * dos) || !grow(&s.d_present, &s.cap_present, chunk * p.n) ||
+        !grow(&s.d_elog, &s.cap_elog, chunk * p.n * 2) ||
+        !grow(&s.d_idx, &s.cap_idx, chunk * cnt * 2))
+      return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+    void *scratch = device_scratch(d, reconstruct_scratch_bytes(p, slen, cb));
+    bool good =
+        ok(hipMemcpyAsync(s.d_a, h_shards + c0 * cnt * sstride, cb * cnt * sstride,
+                          hipMemcpyHostToDevice, s.stream),
+           "H2D shards") &&
+        ok(hipMemcpyAsync(s.d_idx, h_index + c0 * cnt, cb * cnt * 2, hipMemcpyHostToDevice,
+                          s.stream),
+           "H2D index") &&
+        ok(hipMemsetAsync(s.d_present, 0, cb * p.n, s.stream), "present reset");
+    if (good) {
+      hipLaunchKernelGGL(scatter_present, dim3(unsigned(cnt), unsigned(cb)), dim3(256), 0, s.stream,
+                         s.d_a, uint64_t(sstride), s.d_idx, uint32_t(cnt), uint64_t(slen), s.d_b,
+                         uint64_t(dss), uint32_t(nv), s.d_present, uint32_t(p.n));
+      good = ok(hipGetLastError(), "scatter launch") &&
+             ok(launch_error_locator(p, s.d_present, cb, fold, s.d_elog, nullptr, s.stream),
+                "error locator launch") &&
+             ok(launch_reconstruct(p, device_tables(d), s.d_b, slen, dss, s.d_present, s.d_elog, cb,
+                                   s.d_c, dos, scratch, s.stream),
+                "reconstruct launch") &&
+             ok(out_lin ? hipMemcpyAsync(h_out + c0 * ostride, s.d_c, (cb - 1) * ostride + ob,
+                                         hipMemcpyDeviceToHost, s.stream)
+                        : hipMemcpy2DAsync(h_out + c0 * ostride, ostride, s.d_c, ob, ob, cb,
+                                           hipMemcpyDeviceToHost, s.stream),
+                "D2H payloads");
+    }
+    if (!good) return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  }
+  for (Slot &s : pl->slot)
+    if (!ok(hipStreamSynchronize(s.stream), "reconstruct_host_batch"))
+      return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  return res(NPRS_RESULT_OK);
+}
+
+}  // extern "C"

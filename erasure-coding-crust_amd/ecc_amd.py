@@ -116,6 +116,11 @@ def lib():
             "ECCR_AMD_error_locator": (NPRSResult, [ul, vp, ul, vp, vp]),
             "ECCR_AMD_reconstruct_batch": (NPRSResult, [ul, vp, ul, ul, vp, vp, ul, vp, ul, vp]),
             "ECCR_AMD_systematic_batch": (NPRSResult, [ul, vp, ul, ul, ul, vp, ul, vp]),
+            "ECCR_AMD_host_alloc": (vp, [ul]),
+            "ECCR_AMD_host_free": (None, [vp]),
+            "ECCR_AMD_encode_host_batch": (NPRSResult, [ul, vp, ul, ul, ul, vp, ul, ul]),
+            "ECCR_AMD_reconstruct_host_batch": (NPRSResult, [ul, vp, ul, ul, vp, ul, ul, vp, ul,
+                                                             ul]),
             "ECCR_AMD_last_error": (C.c_char_p, []),
         }
         for name, (res, args) in sig.items():
@@ -232,8 +237,12 @@ def measure_performance(nv: int, payload: bytes):
 
 
 def _p(x):
-    """device pointer of a torch tensor (or an int)."""
-    return C.c_void_p(x if isinstance(x, int) else x.data_ptr())
+    """pointer of a torch tensor, a numpy array or an int."""
+    if isinstance(x, int):
+        return C.c_void_p(x)
+    if hasattr(x, "data_ptr"):
+        return C.c_void_p(x.data_ptr())
+    return C.c_void_p(x.ctypes.data)
 
 
 def _stream(stream):
@@ -266,3 +275,24 @@ def systematic_batch(nv, d_shards, shard_len_, shard_stride, batch, d_out, out_s
     _check(lib().ECCR_AMD_systematic_batch(nv, _p(d_shards), shard_len_, shard_stride, batch,
                                            _p(d_out), out_stride, _stream(stream)),
            "systematic_batch")
+
+
+# --------------------------------------------------- host batches (ec_amd.h)
+
+
+def encode_host_batch(nv, h_payloads, payload_len, payload_stride, batch, h_shards, shard_stride,
+                      chunk=0):
+    """payloads [batch][payload_stride] (host) -> shards [batch][nv][shard_stride] (host)."""
+    _check(lib().ECCR_AMD_encode_host_batch(nv, _p(h_payloads), payload_len, payload_stride,
+                                            batch, _p(h_shards), shard_stride, chunk),
+           "encode_host_batch")
+
+
+def reconstruct_host_batch(nv, h_shards, shard_len_, shard_stride, h_index, count, batch, h_out,
+                           out_stride, chunk=0):
+    """present shards compacted [batch][count][shard_stride] + uint16 indices
+    [batch][count] (host) -> payload bytes [batch][out_stride] (host)."""
+    _check(lib().ECCR_AMD_reconstruct_host_batch(nv, _p(h_shards), shard_len_, shard_stride,
+                                                 _p(h_index), count, batch, _p(h_out), out_stride,
+                                                 chunk),
+           "reconstruct_host_batch")

@@ -71,6 +71,33 @@ struct NPRSResult ECCR_AMD_systematic_batch(unsigned long n_validators, const ui
                                             unsigned long out_stride, void *stream);
 
 /* Last error message of the calling thread ("" if none). */
+/* ---- host-resident batches --------------------------
+ * Stream a host batch through the device in chunks of `chunk` payloads (0 =
+ * 64), three chunks in flight (H2D / kernels / D2H overlap).  Synchronous:
+ * returns when the output is in host memory.  Host buffers should come from
+ * ECCR_AMD_host_alloc (pinned) for full PCIe rate. */
+void *ECCR_AMD_host_alloc(unsigned long bytes);
+void ECCR_AMD_host_free(void *ptr);
+
+/* payloads [batch][payload_stride] -> shards [batch][n_validators][shard_stride] */
+struct NPRSResult ECCR_AMD_encode_host_batch(unsigned long n_validators, const uint8_t *h_payloads,
+                                             unsigned long payload_len,
+                                             unsigned long payload_stride, unsigned long batch,
+                                             uint8_t *h_shards, unsigned long shard_stride,
+                                             unsigned long chunk);
+
+/* `count` present shards per payload, compacted: h_shards [batch][count][shard_stride]
+ * with their validator indices h_index [batch][count] (a repeated index counts
+ * once and must carry identical bytes) -> h_out [batch][out_stride >= shard_len*k].
+ * Errors as ECCR_reconstruct: CHUNK_INDEX_OUT_OF_BOUNDS, NOT_ENOUGH_CHUNKS (< k
+ * distinct), UNEVEN_LENGTH. */
+struct NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long n_validators,
+                                                  const uint8_t *h_shards, unsigned long shard_len,
+                                                  unsigned long shard_stride,
+                                                  const uint16_t *h_index, unsigned long count,
+                                                  unsigned long batch, uint8_t *h_out,
+                                                  unsigned long out_stride, unsigned long chunk);
+
 const char *ECCR_AMD_last_error(void);
 
 #ifdef __cplusplus

@@ -119,3 +119,23 @@ def test_no_gpu_fails_loudly():
         E.obtain_chunks(6, b"some payload")
     assert e.value.tag == E.Tag.UNKNOWN_CODE_PARAM
     assert "no HIP device" in E.last_error()
+
+
+def test_host_batch_validation():  # host-batch errors are raised before any device work
+    import numpy as np
+    sh = np.zeros((2, 3, 8), dtype=np.uint8)
+    out = np.zeros((2, 16), dtype=np.uint8)
+    idx = np.array([[0, 1, 7], [0, 1, 2]], dtype=np.uint16)  # 7 >= n_validators 6
+    with pytest.raises(E.ECError) as e:
+        E.reconstruct_host_batch(6, sh, 8, 8, idx, 3, 2, out, 16)
+    assert e.value.tag == E.Tag.CHUNK_INDEX_OUT_OF_BOUNDS and e.value.detail == (7, 6)
+    dup = np.array([[3, 3, 3], [0, 1, 2]], dtype=np.uint16)  # one distinct shard < k = 2
+    with pytest.raises(E.ECError) as e:
+        E.reconstruct_host_batch(6, sh, 8, 8, dup, 3, 2, out, 16)
+    assert e.value.tag == E.Tag.NOT_ENOUGH_CHUNKS
+    with pytest.raises(E.ECError) as e:
+        E.reconstruct_host_batch(6, sh, 7, 8, idx, 3, 2, out, 16)
+    assert e.value.tag == E.Tag.UNEVEN_LENGTH
+    with pytest.raises(E.ECError) as e:
+        E.encode_host_batch(6, np.zeros(4, np.uint8), 0, 4, 1, np.zeros(8, np.uint8), 8)
+    assert e.value.tag == E.Tag.BAD_PAYLOAD

@@ -188,3 +188,25 @@ def test_batch_systematic():
     o = d_out.cpu().numpy()
     for b in range(batch):
         assert o[b][:plen].tobytes() == pay[b].tobytes()
+
+
+# ---------------------------------------------------------------- host batches (row f2)
+@pytest.mark.parametrize("nv,plen,batch,chunk", [(1024, 70001, 7, 2), (100, 5000, 5, 0),
+                                                 (1024, 1_000_000, 4, 3)])
+def test_host_batch_roundtrip(oracle, nv, plen, batch, chunk):
+    n, k, thr = E.code_params(nv)
+    sl = E.shard_len(nv, plen)
+    pay = np.stack([synth.payload(500 + b, plen) for b in range(batch)])
+    sh = np.zeros((batch, nv, sl), dtype=np.uint8)
+    E.encode_host_batch(nv, pay, plen, plen, batch, sh, sl, chunk)
+    for b in (0, batch - 1):
+        assert b"".join(oracle.encode(nv, pay[b].tobytes())) == sh[b].tobytes(), b
+    cnt = thr
+    idx = np.stack([np.sort(synth.present_set(700 + b, nv, cnt)) for b in range(batch)]).astype(np.uint16)
+    idx[0, -1] = idx[0, 0]  # a repeated index counts once (cnt - 1 >= k distinct)
+    comp = np.stack([sh[b][idx[b]] for b in range(batch)])
+    out = np.zeros((batch, sl * k), dtype=np.uint8)
+    E.reconstruct_host_batch(nv, comp, sl, sl, idx, cnt, batch, out, sl * k, chunk)
+    for b in range(batch):
+        assert out[b][:plen].tobytes() == pay[b].tobytes(), b
+        assert not out[b][plen:].any()
