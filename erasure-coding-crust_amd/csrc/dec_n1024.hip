@@ -21,6 +21,14 @@
 #include "ec_device.hpp"
 #include "ec_kernels.hpp"
 
+// DEC_ABL: ablation switches for scripts/micro/dec_ablate.cpp only (results are
+// wrong when set): 1 = no phase-1 shard loads, 2 = phase-1 tables from LDS,
+// 4 = no output stores, 8 = no phase-5 shard re-reads, 16 = no E-out table fill,
+// 32 = one table load per FFT pass.
+#ifndef DEC_ABL
+#define DEC_ABL 0
+#endif
+
 namespace ecamd {
 namespace {
 
@@ -46,6 +54,7 @@ __device__ __forceinline__ uint32_t raddr(uint32_t v) {
 }
 
 __device__ __forceinline__ void lds_tab(const uint8_t *base, uint32_t idx, Tab &T) {
+  if ((DEC_ABL & 32) && idx > 7) return;
   Tabs::load(base, idx, T);
 }
 
@@ -170,7 +179,10 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         const uint8_t *row = SH + uint64_t(v) * sstride + 2 * col0;
         uint32_t w[16];
         const uint64_t avail = slen - 2 * col0;  // bytes of this row inside the tile
-        if (avail >= 64) {
+        if (DEC_ABL & 1) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) w[q] = v * 0x01010101u + q;
+        } else if (avail >= 64) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const uint4 d = reinterpret_cast<const uint4 *>(row)[q];
@@ -185,7 +197,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
           for (uint64_t e = 0; e < avail; ++e) w[e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
         }
         Tab T;
-        load_tab(t.mtab, mul_index(E[v]), T);
+        if (DEC_ABL & 2) Tabs::load(tabs, v & 1023, T);
+        else load_tab(t.mtab, mul_index(E[v]), T);
 #pragma unroll
         for (int g = 0; g < 8; ++g) {  // columns 4g..4g+3: words (h0 l0 h1 l1)(h2 l2 h3 l3)
           const uint32_t a = w[2 * g], c = w[2 * g + 1];
@@ -299,7 +312,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       }
     }
     __syncthreads();  // every wave is done with its region: reuse them for E[y] tables
-    OutTabs::fill(regions, t.mtab, K, [&](uint32_t y) { return mul_index(E[y]); }, tid, THREADS);
+    if (!(DEC_ABL & 16))
+      OutTabs::fill(regions, t.mtab, K, [&](uint32_t y) { return mul_index(E[y]); }, tid, THREADS);
     {
       // q bit0 = p6, bit1 = p7; lane bits = p0..p5.  Positions < 256 only.
       auto fb = [&](int a, int bb, const Tab &T) {
@@ -389,7 +403,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       for (int q = 0; q < 4; ++q) {
         const uint32_t y = 4 * lane + q;
         ol[q] = oh[q] = 0;
-        if (int(y) < nv && pr[y]) {
+        if (!(DEC_ABL & 8) && int(y) < nv && pr[y]) {
           const uint8_t *row = SH + uint64_t(y) * sstride + 2 * cbase;
           uint32_t a = 0, c = 0;
           if (cbase + 4 <= ncols) {
@@ -419,7 +433,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
                             (vperm(ol[1], oh[1], 0x0c0c0400u + 0x0101u * c) << 16);
         const uint32_t w1 = vperm(ol[2], oh[2], 0x0c0c0400u + 0x0101u * c) |
                             (vperm(ol[3], oh[3], 0x0c0c0400u + 0x0101u * c) << 16);
-        *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);
+        if (!(DEC_ABL & 4)) *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);
+        else if (w0 == 0x12345678u && w1 == 0x9abcdef0u) O[0] = 1;  // keep the result live
       }
     }
   }

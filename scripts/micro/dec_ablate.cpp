@@ -1,0 +1,52 @@
+// Reconstruct-kernel ablation timer: dec_n1024.hip compiled with -DDEC_ABL=<mask>
+// (switch list there); 512 x 1 MB payloads, n_validators = 1024, 342 present.
+#include "../../erasure-coding-crust_amd/csrc/dec_n1024.hip"
+
+#include <cstdio>
+#include <vector>
+
+int main() {
+  using namespace ecamd;
+  const Field &F = field();
+  CodeParams p;
+  code_params(1024, &p);
+  uint16_t *sk;
+  MulTab *mt;
+  (void)hipMalloc(&sk, F.skews.size() * 2);
+  (void)hipMalloc(&mt, F.mtab.size() * sizeof(MulTab));
+  (void)hipMemcpy(sk, F.skews.data(), F.skews.size() * 2, hipMemcpyHostToDevice);
+  (void)hipMemcpy(mt, F.mtab.data(), F.mtab.size() * sizeof(MulTab), hipMemcpyHostToDevice);
+  DevTables t;
+  t.skews = sk;
+  t.mtab = mt;
+  const size_t B = 512, plen = 1000000, sl = shard_len(p.k, plen), ss = (sl + 63) / 64 * 64;
+  std::vector<uint8_t> pres(B * 1024, 0);
+  std::vector<uint16_t> el(B * 1024);
+  for (size_t b = 0; b < B; ++b)
+    for (int v = 0; v < 1024; ++v) {
+      pres[b * 1024 + v] = ((v * 2654435761u + b * 97) >> 7) % 3 == 0;  // ~1/3 present
+      el[b * 1024 + v] = uint16_t((v * 40503u + b) % 65535);
+    }
+  uint8_t *sh, *dp, *out;
+  uint16_t *de;
+  (void)hipMalloc(&sh, B * 1024 * ss);
+  (void)hipMalloc(&dp, B * 1024);
+  (void)hipMalloc(&de, B * 1024 * 2);
+  (void)hipMalloc(&out, B * sl * 256);
+  (void)hipMemset(sh, 0x3c, B * 1024 * ss);
+  (void)hipMemcpy(dp, pres.data(), pres.size(), hipMemcpyHostToDevice);
+  (void)hipMemcpy(de, el.data(), el.size() * 2, hipMemcpyHostToDevice);
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  for (int i = 0; i < 2; ++i) launch_reconstruct_n1024(p, t, sh, sl, ss, dp, de, B, out, sl * 256, nullptr);
+  (void)hipEventRecord(a);
+  const int reps = 10;
+  for (int i = 0; i < reps; ++i) launch_reconstruct_n1024(p, t, sh, sl, ss, dp, de, B, out, sl * 256, nullptr);
+  (void)hipEventRecord(b);
+  (void)hipEventSynchronize(b);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, a, b);
+  printf("DEC_ABL=%d  %.4f ms per launch (512 x 1 MB)\n", DEC_ABL, ms / reps);
+  return 0;
+}
