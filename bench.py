@@ -85,11 +85,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # ECCR_BENCH_BACKEND=gloo (rehearsal only): ranks may share a GPU, the
+    # barrier / max-timing run on CPU tensors.  Default: one rank per GPU, RCCL.
+    backend = os.environ.get("ECCR_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     assert E.lib().ECCR_AMD_init_device().tag == 0, E.last_error()
 
     nv, plen, B = args.nv, args.payload, args.batch
@@ -140,7 +148,7 @@ def main():
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
-    elapsed = sharding.max_over_ranks(t1 - t0, dist, dev)
+    elapsed = sharding.max_over_ranks(t1 - t0, dist, dev if backend == "nccl" else None)
 
     # sanity: the last step's reconstruction equals the payloads (round trip)
     ok = bool(torch.equal(d_out[:, :plen], d_pay))
