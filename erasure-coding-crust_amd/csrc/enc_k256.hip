@@ -22,7 +22,8 @@
 
 // ENC_ABL: ablation switches for scripts/micro/enc_ablate.cpp only (results are
 // wrong when set): 1 = no shard stores, 2 = one table load per pass,
-// 4 = no exchanges, 8 = no staging/stores at all.
+// 4 = no exchanges, 8 = no staging/stores at all, 16 = staging reads kept but
+// no global stores.
 #ifndef ENC_ABL
 #define ENC_ABL 0
 #endif
@@ -288,7 +289,9 @@ __device__ __forceinline__ void store_rows(const uint8_t *stg, uint8_t *SH, uint
     const uint32_t shard = s0 + v;
     if (int(shard) >= nv) continue;
     uint8_t *dst = SH + uint64_t(shard) * sstride + 2 * p;
-    if (p + 4 <= npieces) {
+    if (ENC_ABL & 16) {  // ablation: LDS reads kept, global store skipped
+      if (val.x == 0x12345678u && val.y == 0x9abcdef0u) *dst = 1;
+    } else if (p + 4 <= npieces) {
       *reinterpret_cast<uint2 *>(dst) = val;
     } else if (p < npieces) {
       const uint32_t w[2] = {val.x, val.y};
