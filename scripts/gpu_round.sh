@@ -16,7 +16,7 @@ step() {  # name timeout cmd...
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 for s in "$@"; do
   case $s in
-    test) step pytest_gpu 900 python -m pytest tests -m gpu -x -q; rc=$?; ok $rc || exit $rc ;;
+    test) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread; rc=$?; ok $rc || exit $rc ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; ok $rc || exit $rc ;;
     bench_small) step bench_small 600 python bench.py --batch 512 --steps 3 --warmup 1 --cpu-seconds 3; rc=$?; ok $rc || exit $rc ;;
     bench) step bench 900 python bench.py; rc=$?; ok $rc || exit $rc ;;
