@@ -36,7 +36,28 @@ constexpr int N = 1024;
 // GP byte-planar groups per lane (registers), WAVES per workgroup.  GP = 1 with
 // 16 waves gives 4 waves/SIMD (<= 128 VGPRs) for latency hiding; the tile is
 // 128 pieces either way.
-constexpr int GP = 1;
+#ifndef ENC_GP
+#define ENC_GP 1
+#endif
+constexpr int GP = ENC_GP;
+#ifndef ENC_DIRECT
+#define ENC_DIRECT 0
+#endif
+constexpr bool kDirect = ENC_DIRECT;
+#ifndef ENC_OWN
+#define ENC_OWN 1
+#endif
+constexpr bool kOwn = ENC_OWN;
+#ifndef ENC_WIDE
+#define ENC_WIDE 1
+#endif
+#if ENC_WIDE
+#define STAGE stage_rows16
+#define STORE store_rows16
+#else
+#define STAGE stage_rows
+#define STORE store_rows
+#endif
 constexpr int WAVES = 16 / GP;
 constexpr int THREADS = 64 * WAVES;
 constexpr int TILE = 8 * GP * WAVES;  // pieces per tile
@@ -56,6 +77,25 @@ __device__ __forceinline__ void lds_tab(const uint8_t *lds, uint32_t idx, Tab &T
   if ((ENC_ABL & 2) && !first) return;
   first = false;
   Tabs::load(lds, idx, T);
+}
+
+// GF(2)-linear part of the swizzled table address (LdsTabs::addr without the
+// plane term): tlin(a | b) = tlin(a) ^ tlin(b) for disjoint a, b.  A table index
+// is (lane part) | (uniform part), so its address is one v_xor of a per-lane
+// base with a wave-uniform value.
+__host__ __device__ constexpr uint32_t tlin(uint32_t idx) {
+  return ((idx >> 4) << 8) | (((idx ^ (idx >> 4) ^ (idx >> 8)) & 15) << 4);
+}
+
+__device__ __forceinline__ void lds_tab_at(const uint8_t *lds, uint32_t lin, Tab &T) {
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(lds + q * Tabs::kPlane + lin);
+    T.t[4 * q] = v.x;
+    T.t[4 * q + 1] = v.y;
+    T.t[4 * q + 2] = v.z;
+    T.t[4 * q + 3] = v.w;
+  }
 }
 
 // skew index of the block holding position pos_a at stage m (additive_fft.hpp:108,126)
@@ -82,12 +122,44 @@ __device__ __forceinline__ void fbfly(State &s, int ra, int rb, const Tab &T) {
   }
 }
 
+// Table loads are software-pipelined: the next butterfly group's table is
+// requested before the current group's multiplies, so a wave keeps one 80-B
+// table load in flight instead of stalling on each (2 x 20 VGPRs).
+#ifndef ENC_PIPE
+#define ENC_PIPE 1
+#endif
+
 // radix-8 pass over 3 consecutive position bits b0..b0+2 held in registers:
 // pos(r) = base | (r << b0).  Inverse: stages b0, b0+1, b0+2.
 __device__ __forceinline__ void ipass3(State &s, const uint8_t *tabs, uint32_t base, int b0,
                                        uint32_t off) {
-  Tab T;
   bool first = true;
+  if constexpr (ENC_PIPE) {
+    Tab Ta, Tb;
+    const uint32_t lb = tlin(base & ~((2u << b0) - 1));  // lane part of every index below
+    const auto i0 = [&](int rr) { return lb ^ tlin(skew_idx(uint32_t(2 * rr) << b0, b0, off)); };
+    const auto i1 = [&](int hh) { return lb ^ tlin(skew_idx(uint32_t(4 * hh) << b0, b0 + 1, off)); };
+    const uint32_t i2 = lb ^ tlin(skew_idx(0, b0 + 2, off));
+    lds_tab_at(tabs, i0(0), Ta);
+    lds_tab_at(tabs, i0(1), Tb);
+    ibfly(s, 0, 1, Ta);
+    lds_tab_at(tabs, i0(2), Ta);
+    ibfly(s, 2, 3, Tb);
+    lds_tab_at(tabs, i0(3), Tb);
+    ibfly(s, 4, 5, Ta);
+    lds_tab_at(tabs, i1(0), Ta);
+    ibfly(s, 6, 7, Tb);
+    lds_tab_at(tabs, i1(1), Tb);
+    ibfly(s, 0, 2, Ta);
+    ibfly(s, 1, 3, Ta);
+    lds_tab_at(tabs, i2, Ta);
+    ibfly(s, 4, 6, Tb);
+    ibfly(s, 5, 7, Tb);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ibfly(s, r, r + 4, Ta);
+    return;
+  }
+  Tab T;
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {  // stage b0: 4 distinct skews
     lds_tab(tabs, skew_idx(base | (uint32_t(2 * rr) << b0), b0, off), T, first);
@@ -107,8 +179,33 @@ __device__ __forceinline__ void ipass3(State &s, const uint8_t *tabs, uint32_t b
 // forward: stages b0+2, b0+1, b0
 __device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t base, int b0,
                                        uint32_t off) {
-  Tab T;
   bool first = true;
+  if constexpr (ENC_PIPE) {
+    Tab Ta, Tb;
+    const uint32_t lb = tlin(base & ~((2u << b0) - 1));  // lane part of every index below
+    const auto i0 = [&](int rr) { return lb ^ tlin(skew_idx(uint32_t(2 * rr) << b0, b0, off)); };
+    const auto i1 = [&](int hh) { return lb ^ tlin(skew_idx(uint32_t(4 * hh) << b0, b0 + 1, off)); };
+    const uint32_t i2 = lb ^ tlin(skew_idx(0, b0 + 2, off));
+    lds_tab_at(tabs, i2, Ta);
+    lds_tab_at(tabs, i1(0), Tb);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) fbfly(s, r, r + 4, Ta);
+    lds_tab_at(tabs, i1(1), Ta);
+    fbfly(s, 0, 2, Tb);
+    fbfly(s, 1, 3, Tb);
+    lds_tab_at(tabs, i0(0), Tb);
+    fbfly(s, 4, 6, Ta);
+    fbfly(s, 5, 7, Ta);
+    lds_tab_at(tabs, i0(1), Ta);
+    fbfly(s, 0, 1, Tb);
+    lds_tab_at(tabs, i0(2), Tb);
+    fbfly(s, 2, 3, Ta);
+    lds_tab_at(tabs, i0(3), Ta);
+    fbfly(s, 4, 5, Tb);
+    fbfly(s, 6, 7, Ta);
+    return;
+  }
+  Tab T;
   lds_tab(tabs, skew_idx(base, b0 + 2, off), T, first);
 #pragma unroll
   for (int r = 0; r < 4; ++r) fbfly(s, r, r + 4, T);
@@ -128,35 +225,35 @@ __device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t b
 // layout C: register bit0 = p6, bit1 = p7, bit2 = p5 (passenger); stages 6, 7
 // have lane-uniform skews.
 __device__ __forceinline__ void ipassC(State &s, const uint8_t *tabs, uint32_t off) {
-  Tab T;
   bool first = true;
-#pragma unroll
-  for (int p7 = 0; p7 < 2; ++p7) {  // stage 6: skew depends on p7
-    lds_tab(tabs, skew_idx(uint32_t(p7) << 7, 6, off), T, first);
-    ibfly(s, 2 * p7, 2 * p7 + 1, T);
-    ibfly(s, 2 * p7 + 4, 2 * p7 + 5, T);
-  }
-  lds_tab(tabs, skew_idx(0, 7, off), T, first);  // stage 7
-  ibfly(s, 0, 2, T);
-  ibfly(s, 1, 3, T);
-  ibfly(s, 4, 6, T);
-  ibfly(s, 5, 7, T);
+  Tab Ta, Tb;
+  lds_tab_at(tabs, tlin(skew_idx(0, 6, off)), Ta);
+  lds_tab_at(tabs, tlin(skew_idx(1u << 7, 6, off)), Tb);
+  ibfly(s, 0, 1, Ta);
+  ibfly(s, 4, 5, Ta);
+  lds_tab_at(tabs, tlin(skew_idx(0, 7, off)), Ta);  // stage 7
+  ibfly(s, 2, 3, Tb);
+  ibfly(s, 6, 7, Tb);
+  ibfly(s, 0, 2, Ta);
+  ibfly(s, 1, 3, Ta);
+  ibfly(s, 4, 6, Ta);
+  ibfly(s, 5, 7, Ta);
 }
 
 __device__ __forceinline__ void fpassC(State &s, const uint8_t *tabs, uint32_t off) {
-  Tab T;
   bool first = true;
-  lds_tab(tabs, skew_idx(0, 7, off), T, first);
-  fbfly(s, 0, 2, T);
-  fbfly(s, 1, 3, T);
-  fbfly(s, 4, 6, T);
-  fbfly(s, 5, 7, T);
-#pragma unroll
-  for (int p7 = 0; p7 < 2; ++p7) {
-    lds_tab(tabs, skew_idx(uint32_t(p7) << 7, 6, off), T, first);
-    fbfly(s, 2 * p7, 2 * p7 + 1, T);
-    fbfly(s, 2 * p7 + 4, 2 * p7 + 5, T);
-  }
+  Tab Ta, Tb;
+  lds_tab_at(tabs, tlin(skew_idx(0, 7, off)), Ta);
+  lds_tab_at(tabs, tlin(skew_idx(0, 6, off)), Tb);
+  fbfly(s, 0, 2, Ta);
+  fbfly(s, 1, 3, Ta);
+  fbfly(s, 4, 6, Ta);
+  fbfly(s, 5, 7, Ta);
+  lds_tab_at(tabs, tlin(skew_idx(1u << 7, 6, off)), Ta);
+  fbfly(s, 0, 1, Tb);
+  fbfly(s, 4, 5, Tb);
+  fbfly(s, 2, 3, Ta);
+  fbfly(s, 6, 7, Ta);
 }
 
 // position held in register r by lane q (0..31) in each layout
@@ -301,6 +398,136 @@ __device__ __forceinline__ void store_rows(const uint8_t *stg, uint8_t *SH, uint
   }
 }
 
+// ---- 16-byte staging (GP = 1): row v = 16 slots of 16 B, slot w = pieces
+// [8w, 8w + 8) of the tile (wave w), half = inst; slots XOR-swizzled by
+// (v >> 3) & 15 so the 16-lane row reads are conflict free (the layout-A
+// writes are 2-way, 8 instructions per shift).
+__device__ __forceinline__ uint32_t saddr16(uint32_t v, uint32_t slot16) {
+  return v * 256 + ((slot16 ^ ((v >> 3) & 15)) << 4);
+}
+
+__device__ __forceinline__ void stage_rows16(const State &s, uint8_t *stg, uint32_t q,
+                                             uint32_t inst, uint32_t wave) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+    *reinterpret_cast<uint2 *>(stg + saddr16(posA(q, r), wave) + 8 * inst) =
+        to_be(s.l[0][r], s.h[0][r]);
+}
+
+// all waves: LDS rows -> shards [s0, s0 + 256); lane = (row-in-4, 16-B chunk),
+// one dwordx4 per lane per row: 4 store instructions per wave per shift.
+__device__ __forceinline__ void store_rows16(const uint8_t *stg, uint8_t *SH, uint64_t sstride,
+                                             uint32_t s0, int nv, uint64_t piece0,
+                                             uint64_t npieces, uint32_t wave, uint32_t lane) {
+  const uint32_t c = lane & 15;
+  const uint64_t p = piece0 + 8 * c;
+  const bool wide = (sstride & 15) == 0;
+#pragma unroll
+  for (int it = 0; it < 256 / (4 * WAVES); ++it) {
+    const uint32_t v = uint32_t(it) * 4 * WAVES + wave * 4 + (lane >> 4);
+    const uint4 val = *reinterpret_cast<const uint4 *>(stg + saddr16(v, c));
+    const uint32_t shard = s0 + v;
+    if (int(shard) >= nv) continue;
+    uint8_t *dst = SH + uint64_t(shard) * sstride + 2 * p;
+    if (p + 8 <= npieces) {
+      if (wide) {
+        *reinterpret_cast<uint4 *>(dst) = val;
+      } else {
+        reinterpret_cast<uint2 *>(dst)[0] = make_uint2(val.x, val.y);
+        reinterpret_cast<uint2 *>(dst)[1] = make_uint2(val.z, val.w);
+      }
+    } else if (p < npieces) {
+      const uint32_t w[4] = {val.x, val.y, val.z, val.w};
+      for (uint64_t e = 0; e < npieces - p; ++e)
+        *reinterpret_cast<uint16_t *>(dst + 2 * e) = uint16_t(w[e >> 1] >> (16 * (e & 1)));
+    }
+  }
+}
+
+// ---- own-region staging (GP = 1): wave w stages its 8 pieces x 256 rows in
+// its own 4 KB exchange region, 16 B per row (half = inst).  Row v sits in
+// 256-byte block v >> 4 at 16-B slot (v ^ (v >> 4) ^ w) & 15: the 16 lanes that
+// read one row from the 16 regions hit 16 distinct slots (conflict free) and
+// the layout-A writes are 2-way.  A wave only ever writes its own region, so
+// the next write needs a barrier only after the other waves' row reads.
+__device__ __forceinline__ uint32_t soff(uint32_t v, uint32_t w) {
+  return ((v >> 4) << 8) | (((v ^ (v >> 4) ^ w) & 15) << 4);
+}
+
+__device__ __forceinline__ void stage_own(const State &s, uint8_t *xch, uint32_t q,
+                                          uint32_t inst, uint32_t wave) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+    *reinterpret_cast<uint2 *>(xch + soff(posA(q, r), wave) + 8 * inst) =
+        to_be(s.l[0][r], s.h[0][r]);
+}
+
+// all waves: rows [s0, s0 + 256) from the 16 regions -> shards; lane =
+// (row-in-4, source wave c = 16-B chunk of pieces [8c, 8c + 8)).
+__device__ __forceinline__ void store_own(const uint8_t *xbase, uint8_t *SH, uint64_t sstride,
+                                          uint32_t s0, int nv, uint64_t piece0,
+                                          uint64_t npieces, uint32_t wave, uint32_t lane) {
+  asm volatile("" : "+v"(lane));  // recomputed here, not kept live across the FFTs
+  const uint32_t c = lane & 15;
+  const uint64_t p = piece0 + 8 * c;
+  const bool wide = (sstride & 15) == 0;
+  const uint8_t *src = xbase + c * XCH_BYTES;
+#pragma unroll
+  for (int it = 0; it < 256 / (4 * WAVES); ++it) {
+    const uint32_t v = uint32_t(it) * 4 * WAVES + wave * 4 + (lane >> 4);
+    const uint4 val = *reinterpret_cast<const uint4 *>(src + soff(v, c));
+    const uint32_t shard = s0 + v;
+    if (int(shard) >= nv) continue;
+    uint8_t *dst = SH + uint64_t(shard) * sstride + 2 * p;
+    if (p + 8 <= npieces) {
+      if (wide) {
+        *reinterpret_cast<uint4 *>(dst) = val;
+      } else {
+        reinterpret_cast<uint2 *>(dst)[0] = make_uint2(val.x, val.y);
+        reinterpret_cast<uint2 *>(dst)[1] = make_uint2(val.z, val.w);
+      }
+    } else if (p < npieces) {
+      const uint32_t w[4] = {val.x, val.y, val.z, val.w};
+      for (uint64_t e = 0; e < npieces - p; ++e)
+        *reinterpret_cast<uint16_t *>(dst + 2 * e) = uint16_t(w[e >> 1] >> (16 * (e & 1)));
+    }
+  }
+}
+
+// registers in layout A -> shards [s0 + 8q, s0 + 8q + 8) straight from the
+// registers: lanes (q, 0) and (q, 1) write 16 contiguous bytes of a row; the
+// L2 merges the 16 waves' pieces into full lines.  No staging, no barriers.
+__device__ __forceinline__ void store_direct(const State &s, uint8_t *SH, uint64_t sstride,
+                                             uint32_t s0, int nv, uint64_t piece0,
+                                             uint64_t npieces, uint32_t q, uint32_t inst,
+                                             uint32_t wave) {
+  const uint64_t p = piece0 + 8 * GP * wave + 4 * GP * inst;
+  const uint32_t row0 = s0 + 8 * q;
+  uint8_t *dst = SH + uint64_t(row0) * sstride + 2 * p;
+  const bool full = p + 4 * GP <= npieces && int(row0 + 8) <= nv;
+  if (full) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+#pragma unroll
+      for (int g = 0; g < GP; ++g)
+        *reinterpret_cast<uint2 *>(dst + 8 * g) = to_be(s.l[g][r], s.h[g][r]);
+      dst += sstride;
+    }
+    return;
+  }
+  for (int r = 0; r < 8; ++r, dst += sstride) {
+    if (int(row0) + r >= nv) break;
+#pragma unroll
+    for (int g = 0; g < GP; ++g) {
+      const uint2 val = to_be(s.l[g][r], s.h[g][r]);
+      const uint64_t pg = p + 4 * g;
+      const uint32_t w[2] = {val.x, val.y};
+      for (uint64_t e = 0; pg + e < npieces && e < 4; ++e)
+        *reinterpret_cast<uint16_t *>(dst + 8 * g + 2 * e) = uint16_t(w[e >> 1] >> (16 * (e & 1)));
+    }
+  }
+}
+
 }  // namespace
 
 __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict__ payloads,
@@ -371,14 +598,25 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     }
 
     // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)
-    lds_barrier();  // previous tile's staging reads are done
-    stage_rows(s, stg, q, inst, wave);
-    lds_barrier();
-    store_rows(stg, SH, sstride, 0, nv, piece0, npieces, wave, lane);
-    lds_barrier();
+    if constexpr (kOwn) {
+      lds_barrier();  // the other waves are done reading this region (last tile)
+      stage_own(s, xch, q, inst, wave);
+      lds_barrier();
+      store_own(stg, SH, sstride, 0, nv, piece0, npieces, wave, lane);
+      __builtin_amdgcn_sched_barrier(0);
+    } else if constexpr (kDirect) {
+      store_direct(s, SH, sstride, 0, nv, piece0, npieces, q, inst, wave);
+    } else {
+      lds_barrier();  // previous tile's staging reads are done
+      STAGE(s, stg, q, inst, wave);
+      lds_barrier();
+      STORE(stg, SH, sstride, 0, nv, piece0, npieces, wave, lane);
+      lds_barrier();
+    }
 
     // ---- IFFT_256 (index 0): passes A (bits 0-2), B (3-5), C (6-7)
     ipass3(s, tabs, posA(q, 0), 0, 0);
+    if constexpr (kOwn) lds_barrier();  // systematic rows read out of the regions
     exchange<LA, LB>(s, xch, xb, q, inst);
     ipass3(s, tabs, posB(q, 0), 3, 0);
     exchange<LB, LC>(s, xch, xb, q, inst);
@@ -395,15 +633,25 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
 #pragma unroll
         for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(s.l[g][r]), "+v"(s.h[g][r]));
       fpassC(s, tabs, sh);
+      if (kOwn) lds_barrier();  // previous coset's rows read out
       exchange<LC, LB>(s, xch, xb, q, inst);
       fpass3(s, tabs, posB(q, 0), 3, sh);
       exchange<LB, LA>(s, xch, xb, q, inst);
       fpass3(s, tabs, posA(q, 0), 0, sh);
-      lds_barrier();  // all waves done with their exchange regions
-      stage_rows(s, stg, q, inst, wave);
-      lds_barrier();
-      store_rows(stg, SH, sstride, sh, nv, piece0, npieces, wave, lane);
-      lds_barrier();
+      if constexpr (kOwn) {
+        stage_own(s, xch, q, inst, wave);
+        lds_barrier();
+        store_own(stg, SH, sstride, sh, nv, piece0, npieces, wave, lane);
+        __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (kDirect) {
+        store_direct(s, SH, sstride, sh, nv, piece0, npieces, q, inst, wave);
+      } else {
+        lds_barrier();  // all waves done with their exchange regions
+        STAGE(s, stg, q, inst, wave);
+        lds_barrier();
+        STORE(stg, SH, sstride, sh, nv, piece0, npieces, wave, lane);
+        lds_barrier();
+      }
     }
   }
 }
