@@ -30,6 +30,21 @@
 #endif
 
 namespace ecamd {
+// DEC_STAMP (diagnostic builds only): per-phase s_memtime deltas summed over
+// the waves into g_dec_stamp[phase] (read by scripts/micro/dec_ablate.cpp).
+#ifdef DEC_STAMP
+__device__ unsigned long long g_dec_stamp[16];
+#define STAMP(i)                                       \
+  do {                                                 \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
+    acc_[i] += now_ - st_;                             \
+    st_ = now_;                                        \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
 namespace {
 
 constexpr int N = 1024;
@@ -38,7 +53,7 @@ constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
 constexpr int COLS = 4 * WAVES;  // shard positions per tile
 using Tabs = LdsTabs<1024>;
-using OutTabs = LdsTabs<256>;
+using OutTabs = LdsTabs<256>;  // output multiply tables E[y], y < 256 (in the regions)
 constexpr int TAB_REGION = Tabs::kBytes;
 constexpr int REG_BYTES = N * 8;  // one wave's group: 1024 x uint2
 constexpr int LDS_BYTES = TAB_REGION + WAVES * REG_BYTES;
@@ -73,17 +88,42 @@ __device__ __forceinline__ void ib(S16 &s, int a, int b, const Tab &T) {
   mul_acc(s.l[b], s.h[b], T, s.l[a], s.h[a]);
 }
 
-// inverse radix-16 pass over position bits b0..b0+3: pos(r) = base | (r << b0)
-__device__ __forceinline__ void ipass4(S16 &s, const uint8_t *tabs, uint32_t base, int b0) {
-  Tab T;
+// GF(2)-linear part of the swizzled table address (LdsTabs::addr minus the
+// plane term): tlin(a | b) = tlin(a) ^ tlin(b) for disjoint a, b, so a table
+// address is a per-lane base XOR a wave-uniform value.
+__host__ __device__ constexpr uint32_t tlin(uint32_t idx) {
+  return ((idx >> 4) << 8) | (((idx ^ (idx >> 4) ^ (idx >> 8)) & 15) << 4);
+}
+
+__device__ __forceinline__ void tab_at(const uint8_t *lds, uint32_t lin, Tab &T) {
+  if ((DEC_ABL & 32) && lin > 0x70) return;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(lds + q * Tabs::kPlane + lin);
+    T.t[4 * q] = v.x;
+    T.t[4 * q + 1] = v.y;
+    T.t[4 * q + 2] = v.z;
+    T.t[4 * q + 3] = v.w;
+  }
+}
+
+// inverse radix-16 pass over position bits b0..b0+3: pos(r) = lane part | (r << b0),
+// lb = tlin(lane part).  15 tables (8 + 4 + 2 + 1), each requested one step
+// ahead of its use so a table load is always in flight behind the multiplies.
+template <int B0>
+__device__ __forceinline__ void ipass4(S16 &s, const uint8_t *tabs, uint32_t lb) {
+  Tab T[2];
+  tab_at(tabs, lb ^ tlin(skew_idx(0, B0)), T[0]);
+  int k = 0;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int d = 1 << t;
 #pragma unroll
-    for (int blk = 0; blk < 16; blk += 2 * d) {  // one skew per block of 2d registers
-      lds_tab(tabs, skew_idx(base | (uint32_t(blk) << b0), b0 + t), T);
+    for (int blk = 0; blk < 16; blk += 2 * d, ++k) {  // one skew per block of 2d registers
+      const int nt = blk + 2 * d < 16 ? t : t + 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
+      if (nt < 4) tab_at(tabs, lb ^ tlin(skew_idx(uint32_t(nblk) << B0, B0 + nt)), T[(k + 1) & 1]);
 #pragma unroll
-      for (int i = 0; i < d; ++i) ib(s, blk + i, blk + i + d, T);
+      for (int i = 0; i < d; ++i) ib(s, blk + i, blk + i + d, T[k & 1]);
     }
   }
 }
@@ -155,6 +195,9 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
 
   Tabs::fill(tabs, t.mtab, 1023, [&](uint32_t i) { return uint32_t(t.skews[i]); }, tid, THREADS);
   __syncthreads();
+#ifdef DEC_STAMP
+  uint64_t st_ = __builtin_amdgcn_s_memtime(), acc_[11] = {};
+#endif
 
   const uint64_t ncols = slen / 2;
   const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);
@@ -168,7 +211,9 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     uint8_t *O = out + b * ostride;
 
     // ---- phase 1: gather + scale rows v = tid, tid + 512 (decode_main:174-177)
+    STAMP(0);
     __syncthreads();  // previous tile's readers of the regions are done
+    STAMP(1);
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const uint32_t v = tid + half * THREADS;
@@ -210,7 +255,9 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       for (int g = 0; g < 8; ++g)
         *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l[g], h[g]);
     }
+    STAMP(2);
     __syncthreads();
+    STAMP(3);
 
     // ---- phase 2: IFFT_1024 on this wave's group
     S16 s;
@@ -221,7 +268,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         s.l[r] = x.x;
         s.h[r] = x.y;
       }
-      ipass4(s, tabs, 16 * lane, 0);
+      ipass4<0>(s, tabs, tlin(16 * lane));
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         *reinterpret_cast<uint2 *>(my + raddr(16 * lane + r)) = make_uint2(s.l[r], s.h[r]);
@@ -236,7 +283,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         s.l[r] = x.x;
         s.h[r] = x.y;
       }
-      ipass4(s, tabs, baseB, 4);
+      ipass4<4>(s, tabs, tlin((lane >> 4) << 8));
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         *reinterpret_cast<uint2 *>(my + raddr(baseB | (r << 4))) = make_uint2(s.l[r], s.h[r]);
@@ -254,21 +301,22 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       s.h[r] = x.y;
     }
     {
-      Tab T;
+      Tab Ta, Tb;  // stage 8: skew depends on p9 only; stage 9: one skew
+      tab_at(tabs, tlin(skew_idx(0, 8)), Ta);
+      tab_at(tabs, tlin(skew_idx(1u << 9, 8)), Tb);
 #pragma unroll
-      for (int p9 = 0; p9 < 2; ++p9) {  // stage 8: skew depends on p9 only
-        lds_tab(tabs, skew_idx(uint32_t(p9) << 9, 8), T);
+      for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi, 4 * hi + 1, Ta);
+      tab_at(tabs, tlin(skew_idx(0, 9)), Ta);
 #pragma unroll
-        for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi + 2 * p9, 4 * hi + 2 * p9 + 1, T);
-      }
-      lds_tab(tabs, skew_idx(0, 9), T);  // stage 9
+      for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi + 2, 4 * hi + 3, Tb);
 #pragma unroll
       for (int hi = 0; hi < 4; ++hi) {
-        ib(s, 4 * hi, 4 * hi + 2, T);
-        ib(s, 4 * hi + 1, 4 * hi + 3, T);
+        ib(s, 4 * hi, 4 * hi + 2, Ta);
+        ib(s, 4 * hi + 1, 4 * hi + 3, Ta);
       }
     }
 
+    STAMP(4);
     // ---- phase 3: formal derivative (poly_encoder.hpp:195-215), closed form,
     // in place: register r only needs partners r | 2^b > r (still original when
     // r is processed in increasing order) and other lanes' original register r
@@ -293,17 +341,19 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       }
     }
 
+    STAMP(5);
     // ---- phase 4: FFT_1024 restricted to outputs < 256 (afft, additive_fft.hpp:121-141)
     uint32_t ql[4], qh[4];  // live registers: r with p8 = p9 = 0 -> q = (p6, p7)
     {
-      Tab T;
-      lds_tab(tabs, skew_idx(0, 9), T);  // stage 9: keep v < 512 (a-side only)
+      Tab T, T8;
+      tab_at(tabs, tlin(skew_idx(0, 9)), T);  // stage 9: keep v < 512 (a-side only)
+      tab_at(tabs, tlin(skew_idx(0, 8)), T8);
 #pragma unroll
       for (int hi = 0; hi < 4; ++hi) {
         mul_acc(s.l[4 * hi + 2], s.h[4 * hi + 2], T, s.l[4 * hi], s.h[4 * hi]);
         mul_acc(s.l[4 * hi + 3], s.h[4 * hi + 3], T, s.l[4 * hi + 1], s.h[4 * hi + 1]);
       }
-      lds_tab(tabs, skew_idx(0, 8), T);  // stage 8: keep v < 256
+      T = T8;  // stage 8: keep v < 256
 #pragma unroll
       for (int hi = 0; hi < 4; ++hi) {
         mul_acc(s.l[4 * hi + 1], s.h[4 * hi + 1], T, s.l[4 * hi], s.h[4 * hi]);
@@ -311,9 +361,11 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         qh[hi] = s.h[4 * hi];
       }
     }
+    STAMP(6);
     __syncthreads();  // every wave is done with its region: reuse them for E[y] tables
     if (!(DEC_ABL & 16))
       OutTabs::fill(regions, t.mtab, K, [&](uint32_t y) { return mul_index(E[y]); }, tid, THREADS);
+    STAMP(7);
     {
       // q bit0 = p6, bit1 = p7; lane bits = p0..p5.  Positions < 256 only.
       auto fb = [&](int a, int bb, const Tab &T) {
@@ -321,15 +373,36 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         ql[bb] ^= ql[a];
         qh[bb] ^= qh[a];
       };
-      Tab T;
-      lds_tab(tabs, skew_idx(0, 7), T);  // stage 7
-      fb(0, 2, T);
-      fb(1, 3, T);
-#pragma unroll
-      for (int p7 = 0; p7 < 2; ++p7) {  // stage 6
-        lds_tab(tabs, skew_idx(uint32_t(p7) << 7, 6), T);
-        fb(2 * p7, 2 * p7 + 1, T);
-      }
+      // table addresses in order of use (lane bits after each swap stage below)
+      const uint32_t hi67 = ((lane >> 4) & 3) << 6, lo = lane & 15;
+      const uint32_t hi47 = ((lane >> 2) & 15) << 4, lo01 = lane & 3;
+      const uint32_t hi27 = lane << 2;
+      auto L = [&](int i) -> uint32_t {
+        switch (i) {
+          case 0: return tlin(skew_idx(0, 7));
+          case 1: return tlin(skew_idx(0, 6));
+          case 2: return tlin(skew_idx(1u << 7, 6));
+          case 3: return tlin(skew_idx(hi67 | lo, 5));
+          case 4: return tlin(skew_idx(hi67 | lo, 4));
+          case 5: return tlin(skew_idx(hi67 | 32u | lo, 4));
+          case 6: return tlin(skew_idx(hi47 | lo01, 3));
+          case 7: return tlin(skew_idx(hi47 | lo01, 2));
+          case 8: return tlin(skew_idx(hi47 | 8u | lo01, 2));
+          case 9: return tlin(skew_idx(hi27, 1));
+          case 10: return tlin(skew_idx(hi27, 0));
+          default: return tlin(skew_idx(hi27 | 2u, 0));
+        }
+      };
+      Tab T[2];
+      tab_at(tabs, L(0), T[0]);
+      tab_at(tabs, L(1), T[1]);
+      fb(0, 2, T[0]);  // stage 7
+      fb(1, 3, T[0]);
+      tab_at(tabs, L(2), T[0]);
+      fb(0, 1, T[1]);  // stage 6
+      tab_at(tabs, L(3), T[1]);
+      fb(2, 3, T[0]);
+      tab_at(tabs, L(4), T[0]);
       // q (p6, p7) <-> lane bits 4, 5 (p4, p5)
       swap_bit(ql[0], ql[1], 4, false);
       swap_bit(qh[0], qh[1], 4, false);
@@ -340,16 +413,13 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       swap_bit(ql[1], ql[3], 5, false);
       swap_bit(qh[1], qh[3], 5, false);
       // now q = (p4, p5); lane bits 0-3 = p0..p3, 4 = p6, 5 = p7
-      const uint32_t hi67 = ((lane >> 4) & 3) << 6;
-      const uint32_t lo = lane & 15;
-      lds_tab(tabs, skew_idx(hi67 | lo, 5), T);  // stage 5
-      fb(0, 2, T);
-      fb(1, 3, T);
-#pragma unroll
-      for (int p5 = 0; p5 < 2; ++p5) {  // stage 4
-        lds_tab(tabs, skew_idx(hi67 | (uint32_t(p5) << 5) | lo, 4), T);
-        fb(2 * p5, 2 * p5 + 1, T);
-      }
+      fb(0, 2, T[1]);  // stage 5
+      fb(1, 3, T[1]);
+      tab_at(tabs, L(5), T[1]);
+      fb(0, 1, T[0]);  // stage 4
+      tab_at(tabs, L(6), T[0]);
+      fb(2, 3, T[1]);
+      tab_at(tabs, L(7), T[1]);
       // q (p4, p5) <-> lane bits 2, 3 (p2, p3)
       const bool l2 = (lane >> 2) & 1, l3 = (lane >> 3) & 1;
       swap_bit(ql[0], ql[1], 2, l2);
@@ -361,16 +431,13 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       swap_bit(ql[1], ql[3], 3, l3);
       swap_bit(qh[1], qh[3], 3, l3);
       // now q = (p2, p3); lane bits 0,1 = p0,p1; 2,3 = p4,p5; 4,5 = p6,p7
-      const uint32_t hi47 = (((lane >> 2) & 15) << 4);
-      const uint32_t lo01 = lane & 3;
-      lds_tab(tabs, skew_idx(hi47 | lo01, 3), T);  // stage 3
-      fb(0, 2, T);
-      fb(1, 3, T);
-#pragma unroll
-      for (int p3 = 0; p3 < 2; ++p3) {  // stage 2
-        lds_tab(tabs, skew_idx(hi47 | (uint32_t(p3) << 3) | lo01, 2), T);
-        fb(2 * p3, 2 * p3 + 1, T);
-      }
+      fb(0, 2, T[0]);  // stage 3
+      fb(1, 3, T[0]);
+      tab_at(tabs, L(8), T[0]);
+      fb(0, 1, T[1]);  // stage 2
+      tab_at(tabs, L(9), T[1]);
+      fb(2, 3, T[0]);
+      tab_at(tabs, L(10), T[0]);
       // q (p2, p3) <-> lane bits 0, 1 (p0, p1)
       const bool l0 = lane & 1, l1 = (lane >> 1) & 1;
       swap_bit(ql[0], ql[1], 0, l0);
@@ -382,17 +449,15 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       swap_bit(ql[1], ql[3], 1, l1);
       swap_bit(qh[1], qh[3], 1, l1);
       // now q = (p0, p1); lane = (p2 .. p7): y = 4 * lane + q
-      const uint32_t hi27 = lane << 2;
-      lds_tab(tabs, skew_idx(hi27, 1), T);  // stage 1
-      fb(0, 2, T);
-      fb(1, 3, T);
-#pragma unroll
-      for (int p1 = 0; p1 < 2; ++p1) {  // stage 0
-        lds_tab(tabs, skew_idx(hi27 | (uint32_t(p1) << 1), 0), T);
-        fb(2 * p1, 2 * p1 + 1, T);
-      }
+      fb(0, 2, T[1]);  // stage 1
+      fb(1, 3, T[1]);
+      tab_at(tabs, L(11), T[1]);
+      fb(0, 1, T[0]);  // stage 0
+      fb(2, 3, T[1]);
     }
+    STAMP(8);
     __syncthreads();  // E[y] tables in place
+    STAMP(9);
 
     // ---- phase 5: y = 4*lane + q; columns col0 + 4*wave + c (decode_main:185-188,
     // reconstructSub:138-149)
@@ -437,7 +502,12 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         else if (w0 == 0x12345678u && w1 == 0x9abcdef0u) O[0] = 1;  // keep the result live
       }
     }
+    STAMP(10);
   }
+#ifdef DEC_STAMP
+  if ((threadIdx.x & 63) == 0)
+    for (int i = 1; i < 11; ++i) atomicAdd(&g_dec_stamp[i], acc_[i]);
+#endif
 }
 
 bool n1024_applicable(const CodeParams &p) { return p.n == 1024 && p.k == 256; }

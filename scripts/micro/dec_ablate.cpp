@@ -48,5 +48,13 @@ int main() {
   float ms = 0;
   (void)hipEventElapsedTime(&ms, a, b);
   printf("DEC_ABL=%d  %.4f ms per launch (512 x 1 MB)\n", DEC_ABL, ms / reps);
+#ifdef DEC_STAMP
+  unsigned long long st[16];
+  (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_dec_stamp), sizeof(st));
+  unsigned long long tot = 0;
+  for (int i = 1; i <= 10; ++i) tot += st[i];
+  const char *nm[11] = {"", "sync0", "gather", "sync1", "ifft", "deriv", "fft98", "sync2", "fft7-0", "sync3", "output"};
+  for (int i = 1; i <= 10; ++i) printf("  %-8s %5.1f%%\n", nm[i], 100.0 * st[i] / tot);
+#endif
   return 0;
 }
