@@ -38,6 +38,25 @@ METRIC = "device-resident encode+reconstruct GiB/s (and % HBM roofline), n_val=1
 HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+def pmc_traffic(kernel, nv, plen, cnt, batch):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (scripts/pmc_traffic.sh + scripts/pmc_summary.py, newest profiles/rNN),
+    when it was measured on this workload shape; scaled linearly in batch."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")),
+                       reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            w = d["workload"]
+            if (w["n_validators"], w["payload_bytes"], w["present"]) != (nv, plen, cnt):
+                continue
+            return d["kernels"][kernel]["hbm_bytes_per_payload"] * batch, os.path.relpath(path, ROOT)
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
+
+
 def cpu_baseline(nv, plen, cnt, seconds):
     """Single-thread CPU rate of the same path on a bounded sample."""
     import oracle as orc
@@ -162,6 +181,7 @@ def main():
     t_dom, b_dom = kern[dom]
     achieved = b_dom / (t_dom * 1e-3)
 
+    traffic, traffic_src = pmc_traffic(dom, nv, plen, cnt, B)
     total_bytes = world * B * plen * args.steps
     value = total_bytes / elapsed / 2**30
     line = {
@@ -171,13 +191,14 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "u16",
         "data": "synthetic: splitmix64 payloads (seed = payload index), per-payload random "
                 f"{cnt}-of-{nv} present shards",
-        "config": {"workload": f"config2: {plen} B payloads, n_validators={nv}, batch={B}/GPU, "
+        "config": {"workload": f"{'config2: ' if (nv, plen, cnt) == (1024, 1_000_000, 342) else ''}{plen} B payloads, n_validators={nv}, batch={B}/GPU, "
                                f"encode + reconstruct from {cnt} random shards",
                    "n_validators": nv, "payload_bytes": plen, "batch_per_gpu": B,
                    "present_shards": cnt, "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved / 1e9, 2),
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
-                     "traffic": None, "bytes_per_launch": b_dom, "avg_launch_ms": round(t_dom, 4)},
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "bytes_per_launch": b_dom, "avg_launch_ms": round(t_dom, 4)},
         "kernels_ms": {"encode": round(t_enc, 4), "error_locator": round(t_loc, 4),
                        "reconstruct": round(t_rec, 4)},
         "encode_GiBps": round(world * B * plen / (t_enc * 1e-3) / 2**30, 3),

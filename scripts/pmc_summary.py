@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_traffic.sh)
+into per-launch HBM bytes for the codec kernels of the default bench workload.
+
+Corrections (/opt/skills/guides/MI355X_MICROARCH.md, HBM section, and our own
+calibration scripts/micro/fetchcal.hip, profiles/r01/fetchcal.txt): the counters
+are in KiB summed over the TCC instances.  FETCH_SIZE reports half the bytes of
+16-B-per-lane and 8-B-per-lane coalesced reads (x2), and 1.043x the bytes of the
+reconstruct kernel's 64-B-per-lane row reads (/1.043).  WRITE_SIZE is exact for
+the 16-B-per-lane stores.
+  encode:       fetch = raw x 2 (payload reads are 16 B per lane)
+  reconstruct:  fetch = (raw - p5/2) / 1.043 + p5, where p5 = the phase-5
+                8-B-per-lane re-reads of present data rows y < k, known exactly
+                from the workload: B x (present rows < k) x shard_len.
+usage: pmc_summary.py SRC DST B NV PAYLOAD PRESENT
+"""
+import csv
+import collections
+import json
+import sys
+
+src, dst = sys.argv[1], sys.argv[2]
+B, NV, P, CNT = (int(x) for x in sys.argv[3:7])
+N = 1 << (NV - 1).bit_length()
+thr = (NV - 1) // 3 + 1
+K = 1 << (thr.bit_length() - 1)
+SL = ((P + 2 * K - 1) // (2 * K)) * 2
+KERNELS = {"encode_k256": "encode", "reconstruct_n1024": "reconstruct",
+           "encode_g": "encode", "reconstruct_g": "reconstruct", "error_locator_g": "error_locator"}
+
+
+def per_launch(path, counter):
+    val = collections.defaultdict(float)
+    name = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        val[r["Dispatch_Id"]] += float(r["Counter_Value"])
+        name[r["Dispatch_Id"]] = r["Kernel_Name"]
+    out = collections.defaultdict(list)
+    for d, v in val.items():
+        for k, short in KERNELS.items():
+            if k + "(" in name[d]:
+                out[short].append(v * 1024.0)
+    return {k: sum(v) / len(v) for k, v in out.items()}
+
+
+fetch = per_launch(f"{src}/FETCH_SIZE/run_counter_collection.csv", "FETCH_SIZE")
+write = per_launch(f"{src}/WRITE_SIZE/run_counter_collection.csv", "WRITE_SIZE")
+p5 = B * (CNT * K / N) * SL  # expected phase-5 re-read bytes (present rows < k)
+res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, kernel-trace only",
+       "workload": {"batch": B, "n_validators": NV, "payload_bytes": P, "present": CNT,
+                    "shard_len": SL},
+       "corrections": __doc__.split("usage:")[0].strip(), "kernels": {}}
+for k in sorted(set(fetch) | set(write)):
+    f, w = fetch.get(k, 0.0), write.get(k, 0.0)
+    if k == "reconstruct":
+        fc = (f - p5 / 2) / 1.043 + p5
+    else:
+        fc = 2 * f
+    res["kernels"][k] = {"fetch_raw_bytes": round(f), "fetch_bytes": round(fc),
+                         "write_bytes": round(w), "hbm_bytes": round(fc + w),
+                         "hbm_bytes_per_payload": round((fc + w) / B)}
+json.dump(res, open(dst, "w"), indent=1)
+print(json.dumps(res["kernels"], indent=1))
