@@ -296,6 +296,7 @@ int groups_for(uint32_t size) {  // byte-planar groups per workgroup
 }  // namespace
 
 size_t encode_scratch_bytes(const CodeParams &p, size_t plen, size_t batch) {
+  if (k1024_applicable(p)) return k1024_scratch_bytes(plen, batch);
   if (p.k <= uint32_t(kLdsSlots)) return 0;
   const size_t pieces = shard_len(p.k, plen) / 2;
   const size_t tiles = (pieces + 3) / 4;
@@ -311,6 +312,8 @@ hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t 
                        (batch == 1 || pstride % 16 == 0) && sstride % 8 == 0;
   if (aligned && k256_applicable(p))
     return launch_encode_k256(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
+  if (aligned && scratch && k1024_applicable(p))
+    return launch_encode_k1024(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
   const size_t sl = shard_len(p.k, plen);
   const int G = groups_for(p.k);
   const size_t tiles = (sl / 2 + 4 * G - 1) / (4 * G);

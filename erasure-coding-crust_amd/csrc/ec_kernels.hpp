@@ -44,6 +44,14 @@ hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uin
                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                               size_t sstride, hipStream_t s);
 
+// specialised kernels (enc_k1024.hip): k = 1024, n = 4096, needs a coefficient
+// scratch of k1024_scratch_bytes
+bool k1024_applicable(const CodeParams &p);
+size_t k1024_scratch_bytes(size_t plen, size_t batch);
+hipError_t launch_encode_k1024(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
+                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
+                               size_t sstride, void *scratch, hipStream_t s);
+
 // specialised kernels (dec_n1024.hip)
 bool n1024_applicable(const CodeParams &p);
 hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
