@@ -1,0 +1,284 @@
+// dec_n4096.hip — reconstruct specialised for n = 4096, k = 1024
+// (n_validators 3070..4096; BASELINE config 4).
+//
+// decode_main (poly_encoder.hpp:164-189) at n = 4096 per codeword (shard
+// column): IFFT_4096 of the locator-scaled received word, formal derivative,
+// FFT_4096 of which the k = 1024 outputs y < k are read.  Structure used:
+//  * IFFT_4096 stages 0..9 act inside each quarter q (positions 1024q ..
+//    1024q + 1023) with skew indices 1024q + (0..1022): four IFFT_1024 (tf1024.hpp)
+//    with per-quarter tables, then stages 10 and 11 across the quarters in
+//    registers (skews 1023 / 3071 and 2047);
+//  * the derivative in closed form c'[j] = c[j] ^ XOR_{b: j_b = 0} c[j | 2^b]
+//    (poly_encoder.hpp:195-215), in place over the 64 registers and the lane bits;
+//  * FFT stages 11 and 10 only on the side that reaches y < 1024, then one
+//    FFT_1024 (index 0) on quarter 0.
+// A wave owns one byte-planar group (4 columns) for the whole tile: 4 quarters
+// x 16 registers in layout C.  The workgroup (8 waves, 32 columns) shares one
+// 80 KB multiply-table set in LDS, reloaded per quarter (3, 2, 1, then 0, which
+// stays for the FFT) and finally replaced by the output tables E[y], y < k.
+#include <hip/hip_runtime.h>
+
+#include "ec_kernels.hpp"
+#include "tf1024.hpp"
+
+namespace ecamd {
+namespace {
+
+using namespace tf;
+constexpr int N = 4096;
+constexpr int K = 1024;
+constexpr int WAVES = 8;
+constexpr int THREADS = 64 * WAVES;
+constexpr int COLS = 4 * WAVES;
+constexpr int LDS_BYTES = Tabs::kBytes + WAVES * REG_BYTES;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+
+__device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ? 0u : c; }
+
+__device__ __forceinline__ uint32_t dpp_up(uint32_t x, int b) {  // value of lane + 2^b (b < 4)
+  switch (b) {
+    case 0: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x101, 0xf, 0xf, true));
+    case 1: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x102, 0xf, 0xf, true));
+    case 2: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x104, 0xf, 0xf, true));
+    default: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x108, 0xf, 0xf, true));
+  }
+}
+
+// value of lane (lane + 2^b) for lanes whose bit b is 0 (others: don't care)
+__device__ __forceinline__ uint32_t from_upper(uint32_t x, int b) {
+  if (b < 4) return dpp_up(x, b);
+  if (b == 4) {
+    auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return r[1];
+  }
+  auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return r[1];
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(THREADS) reconstruct_n4096(
+    const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
+    const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
+    uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t batch, DevTables t) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t *tabs = lds;
+  uint8_t *regions = lds + Tabs::kBytes;
+  const uint32_t tid0 = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid0 >> 6);
+  uint8_t *my = regions + wave * REG_BYTES;
+
+  const uint64_t ncols = slen / 2;
+  const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);
+  const uint64_t total = uint64_t(tiles_pp) * batch;
+  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    uint32_t tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const uint32_t lane = tid & 63;
+    const uint64_t b = tile / tiles_pp;
+    const uint64_t col0 = (tile % tiles_pp) * COLS;
+    const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
+    const uint8_t *pr = present + b * N;
+    const uint16_t *E = elog + b * N;
+    uint8_t *O = out + b * ostride;
+    S16 Q[4];
+
+    // ---- IFFT quarters 3, 2, 1, 0 (quarter 0's tables stay for the FFT)
+#pragma unroll
+    for (int qi = 0; qi < 4; ++qi) {
+      const int q = 3 - qi;
+      lds_barrier();  // every wave is done with the tables and its region
+      Tabs::fill(tabs, t.mtab, K - 1, [&](uint32_t i) { return uint32_t(t.skews[1024 * q + i]); },
+                 tid, THREADS);
+      // gather + scale the quarter's present rows (decode_main:174-177) into
+      // the 8 groups' regions: thread -> rows 1024q + tid, + 512
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const uint32_t vl = tid + half * THREADS, v = 1024 * q + vl;
+        uint32_t l[8], h[8];
+#pragma unroll
+        for (int g = 0; g < 8; ++g) l[g] = h[g] = 0;
+        if (int(v) < nv && pr[v]) {
+          const uint8_t *row = SH + uint64_t(v) * sstride + 2 * col0;
+          uint32_t w[16];
+          const uint64_t avail = slen - 2 * col0;
+          if (avail >= 64) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const uint4 d = reinterpret_cast<const uint4 *>(row)[j];
+              w[4 * j] = d.x;
+              w[4 * j + 1] = d.y;
+              w[4 * j + 2] = d.z;
+              w[4 * j + 3] = d.w;
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) w[j] = 0;
+            for (uint64_t e = 0; e < avail; ++e) w[e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
+          }
+          Tab T;
+          load_tab(t.mtab, mul_index(E[v]), T);
+#pragma unroll
+          for (int g = 0; g < 8; ++g) {
+            const uint32_t a = w[2 * g], c = w[2 * g + 1];
+            const uint32_t xh = vperm(c, a, 0x06040200u), xl = vperm(c, a, 0x07050301u);
+            mul_acc(xl, xh, T, l[g], h[g]);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < 8; ++g)
+          *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(vl)) = make_uint2(l[g], h[g]);
+      }
+      lds_barrier();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(posA(lane, r)));
+        Q[q].l[r] = x.x;
+        Q[q].h[r] = x.y;
+      }
+      ifft1024(Q[q], tabs, my, lane);  // -> layout C
+    }
+
+    // ---- IFFT stages 10 (skews 1023 / 3071) and 11 (skew 2047) across quarters
+    Tab T10a, T10b, T11;
+    load_tab(t.mtab, t.skews[1023], T10a);
+    load_tab(t.mtab, t.skews[3071], T10b);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      Q[1].l[r] ^= Q[0].l[r];
+      Q[1].h[r] ^= Q[0].h[r];
+      mul_acc(Q[1].l[r], Q[1].h[r], T10a, Q[0].l[r], Q[0].h[r]);
+    }
+    load_tab(t.mtab, t.skews[2047], T11);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      Q[3].l[r] ^= Q[2].l[r];
+      Q[3].h[r] ^= Q[2].h[r];
+      mul_acc(Q[3].l[r], Q[3].h[r], T10b, Q[2].l[r], Q[2].h[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        Q[q + 2].l[r] ^= Q[q].l[r];
+        Q[q + 2].h[r] ^= Q[q].h[r];
+        mul_acc(Q[q + 2].l[r], Q[q + 2].h[r], T11, Q[q].l[r], Q[q].h[r]);
+      }
+    }
+
+    // ---- formal derivative, closed form, in place in increasing (q, r) order:
+    // register partners (q, r | 2^rb) and quarter partners (q | 2^qb, r) are
+    // still original when (q, r) is processed; lane partners read the other
+    // lanes' original (q, r).  Bits: lane = p0..p5, r = (p8, p9, p6, p7), q = (p10, p11).
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        uint32_t al = 0, ah = 0;
+#pragma unroll
+        for (int lb = 0; lb < 6; ++lb) {
+          const uint32_t m = ((lane >> lb) & 1) ? 0u : 0xffffffffu;
+          al ^= from_upper(Q[q].l[r], lb) & m;
+          ah ^= from_upper(Q[q].h[r], lb) & m;
+        }
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+          if (!(r & (1 << rb))) {
+            al ^= Q[q].l[r | (1 << rb)];
+            ah ^= Q[q].h[r | (1 << rb)];
+          }
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+          if (!(q & (1 << qb))) {
+            al ^= Q[q | (1 << qb)].l[r];
+            ah ^= Q[q | (1 << qb)].h[r];
+          }
+        Q[q].l[r] ^= al;
+        Q[q].h[r] ^= ah;
+      }
+    }
+
+    // ---- FFT stage 11 (keep v < 2048) and stage 10 (keep v < 1024): a ^= b * s
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      mul_acc(Q[2].l[r], Q[2].h[r], T11, Q[0].l[r], Q[0].h[r]);
+      mul_acc(Q[3].l[r], Q[3].h[r], T11, Q[1].l[r], Q[1].h[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mul_acc(Q[1].l[r], Q[1].h[r], T10a, Q[0].l[r], Q[0].h[r]);
+    // ---- FFT_1024, index 0, on quarter 0 (tables of quarter 0 still resident)
+    fft1024(Q[0], tabs, my, lane);  // -> layout A: y = 16 lane + r
+
+    // ---- output (decode_main:185-188, reconstructSub:138-149): erased y < k
+    // scaled by E[y] (tables now in LDS), present y copied from the shard
+    lds_barrier();  // every wave is done with the FFT tables
+    Tabs::fill(tabs, t.mtab, K, [&](uint32_t y) { return mul_index(E[y]); }, tid, THREADS);
+    lds_barrier();
+    const uint64_t cbase = col0 + 4 * wave;
+    uint32_t ol[16], oh[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t y = 16 * lane + r;
+      ol[r] = oh[r] = 0;
+      if (int(y) < nv && pr[y]) {
+        const uint8_t *row = SH + uint64_t(y) * sstride + 2 * cbase;
+        uint32_t a = 0, c = 0;
+        if (cbase + 4 <= ncols) {
+          const uint2 d = *reinterpret_cast<const uint2 *>(row);
+          a = d.x;
+          c = d.y;
+        } else {
+          for (uint64_t e = 0; e < 2 * (ncols > cbase ? ncols - cbase : 0); ++e) {
+            if (e < 4) a |= uint32_t(row[e]) << (8 * e);
+            else c |= uint32_t(row[e]) << (8 * (e - 4));
+          }
+        }
+        oh[r] = vperm(c, a, 0x06040200u);
+        ol[r] = vperm(c, a, 0x07050301u);
+      } else {
+        Tab T;
+        Tabs::load(tabs, y, T);
+        mul_acc(Q[0].l[r], Q[0].h[r], T, ol[r], oh[r]);
+      }
+    }
+    // column c: y = 16 lane .. 16 lane + 15 -> 32 contiguous bytes (BE symbols)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint64_t col = cbase + c;
+      if (col >= ncols) break;
+      uint32_t wd[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        wd[j] = vperm(ol[2 * j], oh[2 * j], 0x0c0c0400u + 0x0101u * c) |
+                (vperm(ol[2 * j + 1], oh[2 * j + 1], 0x0c0c0400u + 0x0101u * c) << 16);
+      uint8_t *dst = O + (col * K + 16 * lane) * 2;
+      reinterpret_cast<uint4 *>(dst)[0] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+      reinterpret_cast<uint4 *>(dst)[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);
+    }
+  }
+}
+
+bool n4096_applicable(const CodeParams &p) { return p.n == 4096 && p.k == 1024; }
+
+hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
+                                    const uint8_t *d_shards, size_t slen, size_t sstride,
+                                    const uint8_t *d_present, const uint16_t *d_err_log,
+                                    size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&reconstruct_n4096),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e != hipSuccess) return e;
+  }
+  const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
+  const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
+  hipLaunchKernelGGL(reconstruct_n4096, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
+                     uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out,
+                     uint64_t(ostride), int(p.nv), uint32_t(batch), t);
+  return hipGetLastError();
+}
+
+}  // namespace ecamd
