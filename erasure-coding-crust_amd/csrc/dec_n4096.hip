@@ -31,7 +31,7 @@ constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
 constexpr int COLS = 4 * WAVES;
 constexpr int LDS_BYTES = Tabs::kBytes + WAVES * REG_BYTES;
-static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+static_assert(LDS_BYTES <= 160 * 1024 && Tabs::kBytes == kTabImageBytes, "LDS budget");
 
 __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ? 0u : c; }
 
@@ -82,13 +82,13 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n4096(
     uint8_t *O = out + b * ostride;
     S16 Q[4];
 
-    // ---- IFFT quarters 3, 2, 1, 0 (quarter 0's tables stay for the FFT)
-#pragma unroll
-    for (int qi = 0; qi < 4; ++qi) {
-      const int q = 3 - qi;
+    // ---- IFFT quarters 3, 2, 1, 0 (quarter 0's tables stay for the FFT); a
+    // lambda called per quarter so every Q[] index is a constant (a loop the
+    // unroller declines would leave Q in scratch memory)
+    const auto quarter = [&](S16 &Qq, const int q) __attribute__((always_inline)) {
+      __builtin_amdgcn_sched_barrier(0);
       lds_barrier();  // every wave is done with the tables and its region
-      Tabs::fill(tabs, t.mtab, K - 1, [&](uint32_t i) { return uint32_t(t.skews[1024 * q + i]); },
-                 tid, THREADS);
+      Tabs::copy_image<THREADS>(tabs, t.timg + q * kTabImageBytes, tid);  // skews 1024q + i
       // gather + scale the quarter's present rows (decode_main:174-177) into
       // the 8 groups' regions: thread -> rows 1024q + tid, + 512
 #pragma unroll
@@ -129,14 +129,20 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n4096(
           *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(vl)) = make_uint2(l[g], h[g]);
       }
       lds_barrier();
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(posA(lane, r)));
-        Q[q].l[r] = x.x;
-        Q[q].h[r] = x.y;
+        Qq.l[r] = x.x;
+        Qq.h[r] = x.y;
       }
-      ifft1024(Q[q], tabs, my, lane);  // -> layout C
-    }
+      ifft1024(Qq, tabs, my, lane);  // -> layout C
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    quarter(Q[3], 3);
+    quarter(Q[2], 2);
+    quarter(Q[1], 1);
+    quarter(Q[0], 0);
 
     // ---- IFFT stages 10 (skews 1023 / 3071) and 11 (skew 2047) across quarters
     Tab T10a, T10b, T11;
@@ -211,7 +217,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n4096(
     // ---- output (decode_main:185-188, reconstructSub:138-149): erased y < k
     // scaled by E[y] (tables now in LDS), present y copied from the shard
     lds_barrier();  // every wave is done with the FFT tables
-    Tabs::fill(tabs, t.mtab, K, [&](uint32_t y) { return mul_index(E[y]); }, tid, THREADS);
+    Tabs::gather<THREADS>(tabs, t.mtab, [&](uint32_t y) { return mul_index(E[y]); }, tid);
     lds_barrier();
     const uint64_t cbase = col0 + 4 * wave;
     uint32_t ol[16], oh[16];

@@ -110,6 +110,46 @@ struct LdsTabs {
       T.t[4 * q + 3] = v.w;
     }
   }
+  // cooperative copy of a prebuilt image (DevTables::timg) of ENTRIES entries:
+  // every load issued before the first store
+  template <int THREADS>
+  __device__ static __forceinline__ void copy_image(uint8_t *base, const uint8_t *img,
+                                                    uint32_t tid) {
+    constexpr int kChunks = kBytes / 16;
+    static_assert(kChunks % THREADS == 0, "whole chunks per thread");
+    uint4 v[kChunks / THREADS];
+#pragma unroll
+    for (int k = 0; k < kChunks / THREADS; ++k)
+      v[k] = reinterpret_cast<const uint4 *>(img)[tid + k * THREADS];
+#pragma unroll
+    for (int k = 0; k < kChunks / THREADS; ++k)
+      reinterpret_cast<uint4 *>(base)[tid + k * THREADS] = v[k];
+  }
+  // cooperative gather of ENTRIES tables, entry i <- mtab[src(i)], all index
+  // loads then all table loads in flight at once
+  template <int THREADS, typename F>
+  __device__ static __forceinline__ void gather(uint8_t *base, const MulTab *mtab, F src,
+                                                uint32_t tid) {
+    constexpr int kChunks = ENTRIES * 5;
+    constexpr int kPer = (kChunks + THREADS - 1) / THREADS;
+    uint32_t c[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = tid + k * THREADS;
+      c[k] = i < uint32_t(kChunks) ? src(i / 5) : 0u;
+    }
+    uint4 v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = tid + k * THREADS;
+      if (i < uint32_t(kChunks)) v[k] = reinterpret_cast<const uint4 *>(mtab + c[k])[i % 5];
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = tid + k * THREADS;
+      if (i < uint32_t(kChunks)) *reinterpret_cast<uint4 *>(base + addr(i / 5, i % 5)) = v[k];
+    }
+  }
   // cooperative fill: entry i <- mtab[src(i)]
   template <typename F>
   __device__ static __forceinline__ void fill(uint8_t *base, const MulTab *mtab, int count,

@@ -10,9 +10,17 @@
 
 namespace ecamd {
 
+// LDS images of the multiply tables of one 1023-skew set, in the swizzled
+// LdsTabs<1024> layout: set q = skews[1024 q + i], i < 1023 (q = 0..3), i.e.
+// the tables of an FFT / IFFT of size <= 1024 at index 1024 q.  A kernel loads
+// a set with one coalesced 80 KB copy instead of a 1023-entry gather.
+constexpr size_t kTabImageBytes = 5 * 1024 * 16;
+constexpr int kTabImages = 4;
+
 struct DevTables {
   const uint16_t *skews = nullptr;  // 65535
   const MulTab *mtab = nullptr;     // 65536
+  const uint8_t *timg = nullptr;    // kTabImages x kTabImageBytes
 };
 
 // Scratch (global memory) needed by each launch for FFT sizes whose working

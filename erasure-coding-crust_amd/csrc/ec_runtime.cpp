@@ -2,6 +2,7 @@
 #include "ec_runtime.hpp"
 
 #include <cstdio>
+#include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -13,6 +14,7 @@ struct DeviceState {
   int id = -1;
   uint16_t *skews = nullptr;
   MulTab *mtab = nullptr;
+  uint8_t *timg = nullptr;
   std::mutex mu;
   std::map<uint32_t, uint16_t *> fold;
   void *scratch = nullptr;
@@ -61,6 +63,20 @@ DeviceState *device_state() {
                         hipMemcpyHostToDevice),
               "upload mtab"))
     return nullptr;
+  // LDS table images (ec_kernels.hpp kTabImages): LdsTabs<1024>::addr layout
+  std::vector<uint8_t> img(kTabImages * kTabImageBytes, 0);
+  for (int q = 0; q < kTabImages; ++q)
+    for (uint32_t i = 0; i < 1023; ++i) {
+      const uint8_t *src = reinterpret_cast<const uint8_t *>(&f.mtab[f.skews[1024 * q + i]]);
+      const uint32_t sw = (i ^ (i >> 4) ^ (i >> 8)) & 15;
+      for (uint32_t plane = 0; plane < 5; ++plane)
+        std::memcpy(&img[q * kTabImageBytes + plane * 16384 + ((i >> 4) << 8) + (sw << 4)],
+                    src + 16 * plane, 16);
+    }
+  if (!hip_ok(hipMalloc(&st->timg, img.size()), "hipMalloc(table images)") ||
+      !hip_ok(hipMemcpy(st->timg, img.data(), img.size(), hipMemcpyHostToDevice),
+              "upload table images"))
+    return nullptr;
   slot = std::move(st);
   return slot.get();
 }
@@ -69,6 +85,7 @@ DevTables device_tables(DeviceState *d) {
   DevTables t;
   t.skews = d->skews;
   t.mtab = d->mtab;
+  t.timg = d->timg;
   return t;
 }
 

@@ -132,8 +132,7 @@ __global__ void __launch_bounds__(THREADS)
   uint8_t *my = regions + wave * REG_BYTES;
 
   // this transform's 1023 skews (additive_fft.hpp:108,126: skews[j - 1 + index])
-  Tabs::fill(tabs, t.mtab, K - 1, [&](uint32_t i) { return uint32_t(t.skews[shift + i]); }, tid0,
-             THREADS);
+  Tabs::copy_image<THREADS>(tabs, t.timg + (shift / K) * kTabImageBytes, tid0);
   __syncthreads();
 
   const uint64_t npieces = slen / 2;
