@@ -27,7 +27,10 @@ namespace {
 using namespace tf;
 constexpr int N = 4096;
 constexpr int K = 1024;
-constexpr int WAVES = 8;
+#ifndef DEC4_WAVES
+#define DEC4_WAVES 8
+#endif
+constexpr int WAVES = DEC4_WAVES;
 constexpr int THREADS = 64 * WAVES;
 constexpr int COLS = 4 * WAVES;
 constexpr int LDS_BYTES = Tabs::kBytes + WAVES * REG_BYTES;
@@ -57,7 +60,11 @@ __device__ __forceinline__ uint32_t from_upper(uint32_t x, int b) {
 
 }  // namespace
 
-__global__ void __launch_bounds__(THREADS) reconstruct_n4096(
+__global__ void __launch_bounds__(THREADS)
+#if DEC4_WAVES == 4
+__attribute__((amdgpu_waves_per_eu(1, 1)))
+#endif
+reconstruct_n4096(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
     uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t batch, DevTables t) {
@@ -92,7 +99,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n4096(
       // gather + scale the quarter's present rows (decode_main:174-177) into
       // the 8 groups' regions: thread -> rows 1024q + tid, + 512
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
+      for (int half = 0; half < 1024 / THREADS; ++half) {
         const uint32_t vl = tid + half * THREADS, v = 1024 * q + vl;
         uint32_t l[8], h[8];
 #pragma unroll
