@@ -95,7 +95,10 @@ reconstruct_n4096(
     const auto quarter = [&](S16 &Qq, const int q) __attribute__((always_inline)) {
       __builtin_amdgcn_sched_barrier(0);
       lds_barrier();  // every wave is done with the tables and its region
-      Tabs::copy_image<THREADS>(tabs, t.timg + q * kTabImageBytes, tid);  // skews 1024q + i
+      // the quarter's tables (skews 1024q + i) by LDS-DMA, in the background
+      // of the row gather; retired before the barrier below
+      Tabs::dma_image<THREADS>(tabs, t.timg + q * kTabImageBytes, tid);
+      __builtin_amdgcn_sched_barrier(0);
       // gather + scale the quarter's present rows (decode_main:174-177) into
       // the 8 groups' regions: thread -> rows 1024q + tid, + 512
 #pragma unroll
@@ -135,6 +138,7 @@ reconstruct_n4096(
         for (int g = 0; g < 8; ++g)
           *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(vl)) = make_uint2(l[g], h[g]);
       }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // table image landed
       lds_barrier();
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll

@@ -125,6 +125,22 @@ struct LdsTabs {
     for (int k = 0; k < kChunks / THREADS; ++k)
       reinterpret_cast<uint4 *>(base)[tid + k * THREADS] = v[k];
   }
+  // the same copy by LDS-DMA (global_load_lds_dwordx4): no VGPRs, completes in
+  // the background; the caller retires it (s_waitcnt vmcnt(0)) before the
+  // barrier that precedes the first table read.  A wave-instruction writes 1 KB
+  // of LDS linearly, which is exactly the image layout.
+  template <int THREADS>
+  __device__ static __forceinline__ void dma_image(uint8_t *base, const uint8_t *img,
+                                                   uint32_t tid) {
+    constexpr int kChunks = kBytes / 16;
+    static_assert(kChunks % THREADS == 0 && THREADS % 64 == 0, "whole chunks per thread");
+    const uint32_t wave_base = (tid & ~63u) * 16;  // this wave's 1 KB slice
+#pragma unroll
+    for (int k = 0; k < kChunks / THREADS; ++k)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void *)(img + 16 * (tid + k * THREADS)),
+          (__attribute__((address_space(3))) void *)(base + wave_base + k * THREADS * 16), 16, 0, 0);
+  }
   // cooperative gather of ENTRIES tables, entry i <- mtab[src(i)], all index
   // loads then all table loads in flight at once
   template <int THREADS, typename F>
