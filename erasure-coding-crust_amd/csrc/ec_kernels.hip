@@ -312,6 +312,8 @@ hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t 
                        (batch == 1 || pstride % 16 == 0) && sstride % 8 == 0;
   if (aligned && k256_applicable(p))
     return launch_encode_k256(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
+  if (aligned && encgen_applicable(p))
+    return launch_encode_gen(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
   if (aligned && scratch && k1024_applicable(p))
     return launch_encode_k1024(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
   const size_t sl = shard_len(p.k, plen);

@@ -1,0 +1,263 @@
+// enc_gen.hip — register-blocked encode for k = 2^M, M = 5..7 (k = 32, 64,
+// 128) and n <= 1024: n_validators ~96..765, which includes today's Polkadot
+// validator counts (k = 128, n = 1024 for 512..765 validators).
+//
+// The 1024 positions a wave holds (tf1024.hpp: 64 lanes x 16 registers, 4
+// pieces per byte-planar register) are read as 1024 / k independent k-point
+// transforms: position = (instance << M) | local, so a wave encodes
+// 4 * 1024 / k pieces at once.  encodeLow (poly_encoder.hpp:217-240):
+//   IFFT_k  = pass A (stages 0-3, register bits = position bits 0-3) and, after
+//             the A -> B exchange, pass B (stages 4..M-1): ends in layout B;
+//   FFT_k at each coset s = k, 2k, .. < n: pass B (stages M-1..4), B -> A
+//             exchange, pass A (stages 3..0): ends in layout A = shard rows.
+// Stage index arithmetic only sees the local bits (pos & (k-1)); instance bits
+// ride along as extra register / lane bits.  All n - 1 <= 1023 skews of an
+// n <= 1024 code are one LDS table image (set 0); a coset's tables are that
+// image at offset s, folded into the linear table address (tlin).  In layout B
+// every table index is wave-uniform.
+//
+// Shard rows: per coset, k rows x 32 * 1024 / k pieces (64 KB) are staged in the
+// waves' own regions (row v of wave w: 8 * 1024 / k bytes) and stored as 16-B
+// lane chunks of contiguous row segments (64 * 1024 / k bytes).
+#include <hip/hip_runtime.h>
+
+#include "ec_kernels.hpp"
+#include "tf1024.hpp"
+
+namespace ecamd {
+namespace {
+
+using namespace tf;
+constexpr int WAVES = 8;
+constexpr int THREADS = 64 * WAVES;
+constexpr int LDS_BYTES = Tabs::kBytes + WAVES * REG_BYTES;
+static_assert(LDS_BYTES <= 160 * 1024 && Tabs::kBytes == kTabImageBytes, "LDS budget");
+
+template <int M>
+struct Geo {
+  static constexpr uint32_t K = 1u << M;
+  static constexpr int INST = 1024 >> M;  // transforms per wave
+  static constexpr int WP = 4 * INST;     // pieces per wave
+  static constexpr int TP = WAVES * WP;   // pieces per tile
+  static constexpr int ROWB = 2 * WP;     // bytes of one shard row per wave and tile
+};
+
+// inverse pass over register bits 0..NS-1 = position bits B0..B0+NS-1
+template <int B0, int NS, int M>
+__device__ __forceinline__ void ipassg(S16 &s, const uint8_t *tabs, uint32_t lb) {
+  constexpr uint32_t KM = Geo<M>::K - 1;
+  Tab T[2];
+  tab_at(tabs, lb ^ tlin(skew_idx(0, B0)), T[0]);
+  int k = 0;
+#pragma unroll
+  for (int t = 0; t < NS; ++t) {
+    const int d = 1 << t;
+#pragma unroll
+    for (int blk = 0; blk < 16; blk += 2 * d, ++k) {
+      const int nt = blk + 2 * d < 16 ? t : t + 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
+      if (nt < NS)
+        tab_at(tabs, lb ^ tlin(skew_idx((uint32_t(nblk) << B0) & KM, B0 + nt)), T[(k + 1) & 1]);
+#pragma unroll
+      for (int i = 0; i < d; ++i) ib(s, blk + i, blk + i + d, T[k & 1]);
+    }
+  }
+}
+
+template <int B0, int NS, int M>
+__device__ __forceinline__ void fpassg(S16 &s, const uint8_t *tabs, uint32_t lb) {
+  constexpr uint32_t KM = Geo<M>::K - 1;
+  Tab T[2];
+  tab_at(tabs, lb ^ tlin(skew_idx(0, B0 + NS - 1)), T[0]);
+  int k = 0;
+#pragma unroll
+  for (int t = NS - 1; t >= 0; --t) {
+    const int d = 1 << t;
+#pragma unroll
+    for (int blk = 0; blk < 16; blk += 2 * d, ++k) {
+      const int nt = blk + 2 * d < 16 ? t : t - 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
+      if (nt >= 0)
+        tab_at(tabs, lb ^ tlin(skew_idx((uint32_t(nblk) << B0) & KM, B0 + nt)), T[(k + 1) & 1]);
+#pragma unroll
+      for (int i = 0; i < d; ++i) fb(s, blk + i, blk + i + d, T[k & 1]);
+    }
+  }
+}
+
+// layout A rows of the wave -> own region: row local, instance i -> 8 B at
+// row * ROWB + 8 i
+template <int M>
+__device__ __forceinline__ void stage(const S16 &s, uint8_t *my, uint32_t lane) {
+  using Gm = Geo<M>;
+  const uint32_t inst = (16 * lane) >> M, local0 = (16 * lane) & (Gm::K - 1);
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    *reinterpret_cast<uint2 *>(my + (local0 + r) * Gm::ROWB + 8 * inst) = to_be(s.l[r], s.h[r]);
+}
+
+// all waves: rows s0 + v, v < k, from the 8 regions -> shards
+template <int M>
+__device__ __forceinline__ void store_rows(const uint8_t *regions, uint8_t *SH, uint64_t sstride,
+                                           uint32_t s0, int nv, uint64_t piece0, uint64_t npieces,
+                                           uint32_t tid) {
+  using Gm = Geo<M>;
+  constexpr int CPW = Gm::ROWB / 16;      // 16-B chunks per row per wave
+  constexpr int CPR = CPW * WAVES;        // chunks per row
+  constexpr int ITER = Gm::K * CPR / THREADS;
+  static_assert(Gm::K * CPR % THREADS == 0, "whole iterations");
+  const bool wide = (sstride & 15) == 0;
+#pragma unroll 4
+  for (int it = 0; it < ITER; ++it) {
+    const uint32_t ch = uint32_t(it) * THREADS + tid;
+    const uint32_t v = ch / CPR, c16 = ch % CPR;
+    const uint32_t w = c16 / CPW, o = (c16 % CPW) * 16;
+    const uint4 val = *reinterpret_cast<const uint4 *>(regions + w * REG_BYTES + v * Gm::ROWB + o);
+    const uint32_t shard = s0 + v;
+    const uint64_t p = piece0 + 8 * c16;  // first of the chunk's 8 pieces
+    if (int(shard) >= nv || p >= npieces) continue;
+    uint8_t *dst = SH + uint64_t(shard) * sstride + 2 * p;
+    if (p + 8 <= npieces) {
+      if (wide) {
+        *reinterpret_cast<uint4 *>(dst) = val;
+      } else {
+        reinterpret_cast<uint2 *>(dst)[0] = make_uint2(val.x, val.y);
+        reinterpret_cast<uint2 *>(dst)[1] = make_uint2(val.z, val.w);
+      }
+    } else {
+      const uint32_t wd[4] = {val.x, val.y, val.z, val.w};
+      for (uint64_t e = 0; e < npieces - p; ++e)
+        *reinterpret_cast<uint16_t *>(dst + 2 * e) = uint16_t(wd[e >> 1] >> (16 * (e & 1)));
+    }
+  }
+}
+
+template <int M>
+__global__ void __launch_bounds__(THREADS)
+    encode_gen(const uint8_t *__restrict__ payloads, uint64_t plen, uint64_t pstride,
+               uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride, int nv, int n,
+               uint32_t batch, DevTables t) {
+  using Gm = Geo<M>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t *tabs = lds;
+  uint8_t *regions = lds + Tabs::kBytes;
+  const uint32_t tid0 = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid0 >> 6);
+  uint8_t *my = regions + wave * REG_BYTES;
+
+  Tabs::copy_image<THREADS>(tabs, t.timg, tid0);  // skews 0..1022: every coset of n <= 1024
+  __syncthreads();
+
+  const uint64_t npieces = slen / 2;
+  const uint32_t tiles_pp = uint32_t((npieces + Gm::TP - 1) / Gm::TP);
+  const uint64_t total = uint64_t(tiles_pp) * batch;
+  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    uint32_t tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const uint32_t lane = tid & 63;
+    const uint64_t b = tile / tiles_pp;
+    const uint64_t piece0 = (tile % tiles_pp) * Gm::TP;
+    const uint8_t *P = payloads + b * pstride;
+    uint8_t *SH = shards + b * uint64_t(nv) * sstride;
+
+    // ---- load: lane -> positions 16 lane .. + 15 = instance i, locals l0 .. l0 + 15
+    S16 s;
+    {
+      const uint32_t inst = (16 * lane) >> M, local0 = (16 * lane) & (Gm::K - 1);
+      uint32_t D[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t piece = piece0 + uint64_t(Gm::WP) * wave + 4 * inst + u;
+        const uint64_t off = piece * 2 * Gm::K + 2 * local0;
+        if (off + 32 <= plen) {
+          const uint4 a = *reinterpret_cast<const uint4 *>(P + off);
+          const uint4 c = *reinterpret_cast<const uint4 *>(P + off + 16);
+          D[u][0] = a.x; D[u][1] = a.y; D[u][2] = a.z; D[u][3] = a.w;
+          D[u][4] = c.x; D[u][5] = c.y; D[u][6] = c.z; D[u][7] = c.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) D[u][j] = 0;
+          for (uint64_t e = off; e < plen && e < off + 32; ++e)
+            D[u][(e - off) >> 2] |= uint32_t(P[e]) << (8 * ((e - off) & 3));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t t0 = vperm(D[1][j], D[0][j], 0x05010400u), t1 = vperm(D[1][j], D[0][j], 0x07030602u);
+        const uint32_t u0 = vperm(D[3][j], D[2][j], 0x05010400u), u1 = vperm(D[3][j], D[2][j], 0x07030602u);
+        s.h[2 * j] = vperm(u0, t0, 0x05040100u);
+        s.l[2 * j] = vperm(u0, t0, 0x07060302u);
+        s.h[2 * j + 1] = vperm(u1, t1, 0x05040100u);
+        s.l[2 * j + 1] = vperm(u1, t1, 0x07060302u);
+      }
+    }
+
+    // ---- systematic shards 0..k-1 = the data symbols (poly_encoder.hpp:239)
+    lds_barrier();  // the other waves are done reading the regions (last tile)
+    stage<M>(s, my, lane);
+    lds_barrier();
+    store_rows<M>(regions, SH, sstride, 0, nv, piece0, npieces, tid);
+    lds_barrier();
+
+    // ---- IFFT_k (index 0): pass A, exchange, pass B -> layout B
+    const uint32_t lbA = tlin((16 * lane) & (Gm::K - 1));
+    ipassg<0, (M < 4 ? M : 4), M>(s, tabs, lbA);
+    exchange<LA, LB>(s, my, lane);
+    ipassg<4, M - 4, M>(s, tabs, 0);
+    const S16 coef = s;
+
+    // ---- FFT_k at each coset shift (encodeLow, poly_encoder.hpp:229-237)
+    for (int sh = int(Gm::K); sh < n && sh < nv; sh += int(Gm::K)) {
+      s = coef;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(s.l[r]), "+v"(s.h[r]));
+      const uint32_t lo = tlin(uint32_t(sh));  // tables at offset sh (disjoint bits)
+      fpassg<4, M - 4, M>(s, tabs, lo);
+      exchange<LB, LA>(s, my, lane);
+      fpassg<0, (M < 4 ? M : 4), M>(s, tabs, tlin((16 * lane) & (Gm::K - 1)) ^ lo);
+      lds_barrier();  // all waves done with their regions (exchange, previous stores)
+      stage<M>(s, my, lane);
+      lds_barrier();
+      store_rows<M>(regions, SH, sstride, uint32_t(sh), nv, piece0, npieces, tid);
+      lds_barrier();
+    }
+  }
+}
+
+template <int M>
+hipError_t launch_m(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
+                    size_t plen, size_t pstride, size_t batch, uint8_t *d_shards, size_t sstride,
+                    hipStream_t s) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&encode_gen<M>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e != hipSuccess) return e;
+  }
+  const size_t sl = shard_len(p.k, plen);
+  const size_t tiles = (sl / 2 + Geo<M>::TP - 1) / Geo<M>::TP * batch;
+  const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
+  hipLaunchKernelGGL(encode_gen<M>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
+                     uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride),
+                     int(p.nv), int(p.n), uint32_t(batch), t);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool encgen_applicable(const CodeParams &p) {
+  return (p.k == 32 || p.k == 64 || p.k == 128) && p.n <= 1024 && p.n >= 2 * p.k;
+}
+
+hipError_t launch_encode_gen(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
+                             size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
+                             size_t sstride, hipStream_t s) {
+  switch (p.k) {
+    case 32: return launch_m<5>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
+    case 64: return launch_m<6>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
+    default: return launch_m<7>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
+  }
+}
+
+}  // namespace ecamd

@@ -92,7 +92,8 @@ def test_golden_vectors(golden_vectors):
 
 
 # ---------------------------------------------------------------- random sweep vs oracle
-@pytest.mark.parametrize("nv", [2, 3, 5, 6, 7, 9, 16, 33, 100, 255, 1000, 1024, 2048, 3070, 3500, 4096])
+@pytest.mark.parametrize("nv", [2, 3, 5, 6, 7, 9, 16, 33, 100, 200, 255, 300, 384, 600, 700, 1000,
+                                1024, 2048, 3070, 3500, 4096])
 def test_random_vs_oracle(oracle, nv):
     rng = np.random.default_rng(nv)
     n, k, thr = E.code_params(nv)
@@ -154,7 +155,11 @@ def _batch_case(nv, plen, batch, cnt_key="threshold", seed0=0, pad=0):
     (1024, 131073, 2, 64), (1000, 99999, 2, 64), (800, 12345, 3, 64), (4096, 3001, 2, 64),
     # k = 1024 / n = 4096 fast path (config 4): several 64-piece tiles, a partly
     # populated last coset (nv 3500), tight and 8/16/64-byte row pitches
-    (4096, 300001, 2, 64), (3070, 300001, 2, 16), (3500, 131073, 2, 8), (4096, 131072, 1, 0)])
+    (4096, 300001, 2, 64), (3070, 300001, 2, 16), (3500, 131073, 2, 8), (4096, 131072, 1, 0),
+    # k = 32 / 64 / 128, n <= 1024 register-blocked encode: several tiles,
+    # partly populated last cosets, 8/16/64-byte pitches
+    (600, 300001, 2, 64), (700, 5000, 2, 64), (384, 131073, 2, 64), (300, 70001, 3, 16),
+    (100, 12345, 3, 8), (200, 200001, 2, 64)])
 def test_batch_vs_oracle(oracle, nv, plen, batch, pad):
     pay, pres, sh, el, out = _batch_case(nv, plen, batch, pad=pad)
     n, k, _ = E.code_params(nv)
