@@ -1,0 +1,412 @@
+// dec_gen.hip — register-blocked reconstruct for n = 2^L, L = 6..10 (n = 64 ..
+// 1024), any k with 16 <= k < n: the n_validators the n = 1024 / k = 256
+// kernel does not cover (e.g. 512..765 validators: n = 1024, k = 128).
+//
+// As in enc_gen.hip, a wave's 1024 positions (tf1024.hpp: 64 lanes x 16
+// registers, 4 codewords per byte-planar register) are read as 1024 / n
+// independent n-point codewords: position = (instance << L) | local.  Per
+// codeword (decode_main, poly_encoder.hpp:164-189):
+//   gather + scale the present received symbols by the locator E[v] into the
+//   waves' regions (a workgroup tile is 32 * 1024 / n shard columns = 64 KB of
+//   received rows), IFFT_n (passes A / B / C over the local stages), the
+//   formal derivative in closed form c'[j] = c[j] ^ XOR_{b < L: j_b = 0}
+//   c[j | 2^b] in whatever layout the IFFT ended in, the full FFT_n back to
+//   layout A, and y < k out: erased y scaled by E[y] (tables in LDS), present y
+//   copied from the shard.
+// Stage arithmetic only sees the local bits, exactly as the reference's
+// n-point transforms (additive_fft.hpp:99-141, skews at index 0).
+#include <hip/hip_runtime.h>
+
+#include "ec_kernels.hpp"
+#include "tf1024.hpp"
+
+namespace ecamd {
+namespace {
+
+using namespace tf;
+constexpr int WAVES = 8;
+constexpr int THREADS = 64 * WAVES;
+using OutTabs = LdsTabs<512>;  // E[y], y < k <= 512, in the regions
+constexpr int LDS_BYTES = Tabs::kBytes + WAVES * REG_BYTES;
+static_assert(LDS_BYTES <= 160 * 1024 && OutTabs::kBytes <= WAVES * REG_BYTES, "LDS budget");
+
+__device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ? 0u : c; }
+
+__device__ __forceinline__ uint32_t dpp_up(uint32_t x, int b) {  // value of lane + 2^b (b < 4)
+  switch (b) {
+    case 0: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x101, 0xf, 0xf, true));
+    case 1: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x102, 0xf, 0xf, true));
+    case 2: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x104, 0xf, 0xf, true));
+    default: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x108, 0xf, 0xf, true));
+  }
+}
+
+// value of lane (lane + 2^b) for lanes whose bit b is 0 (others: don't care)
+__device__ __forceinline__ uint32_t from_upper(uint32_t x, int b) {
+  if (b < 4) return dpp_up(x, b);
+  if (b == 4) {
+    auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return r[1];
+  }
+  auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return r[1];
+}
+
+// position bit held by register bit t / lane bit u in each layout (tf1024.hpp)
+template <Layout X>
+__host__ __device__ constexpr int reg_pbit(int t) {
+  if constexpr (X == LA) return t;
+  else if constexpr (X == LB) return t + 4;
+  else return t == 0 ? 8 : t == 1 ? 9 : t == 2 ? 6 : 7;
+}
+template <Layout X>
+__host__ __device__ constexpr int lane_pbit(int u) {
+  if constexpr (X == LB) return u < 4 ? u : u + 4;
+  else if constexpr (X == LA) return u + 4;
+  else return u;
+}
+
+// inverse / forward pass over register bits 0..NS-1 (position bits B0..) of
+// the local index pos & (n - 1); lb = tlin of the (masked) lane part
+template <int B0, int NS, int L>
+__device__ __forceinline__ void ipassg(S16 &s, const uint8_t *tabs, uint32_t lb) {
+  constexpr uint32_t NM = (1u << L) - 1;
+  Tab T[2];
+  tab_at(tabs, lb ^ tlin(skew_idx(0, B0)), T[0]);
+  int k = 0;
+#pragma unroll
+  for (int t = 0; t < NS; ++t) {
+    const int d = 1 << t;
+#pragma unroll
+    for (int blk = 0; blk < 16; blk += 2 * d, ++k) {
+      const int nt = blk + 2 * d < 16 ? t : t + 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
+      if (nt < NS)
+        tab_at(tabs, lb ^ tlin(skew_idx((uint32_t(nblk) << B0) & NM, B0 + nt)), T[(k + 1) & 1]);
+#pragma unroll
+      for (int i = 0; i < d; ++i) ib(s, blk + i, blk + i + d, T[k & 1]);
+    }
+  }
+}
+
+template <int B0, int NS, int L>
+__device__ __forceinline__ void fpassg(S16 &s, const uint8_t *tabs, uint32_t lb) {
+  constexpr uint32_t NM = (1u << L) - 1;
+  Tab T[2];
+  tab_at(tabs, lb ^ tlin(skew_idx(0, B0 + NS - 1)), T[0]);
+  int k = 0;
+#pragma unroll
+  for (int t = NS - 1; t >= 0; --t) {
+    const int d = 1 << t;
+#pragma unroll
+    for (int blk = 0; blk < 16; blk += 2 * d, ++k) {
+      const int nt = blk + 2 * d < 16 ? t : t - 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
+      if (nt >= 0)
+        tab_at(tabs, lb ^ tlin(skew_idx((uint32_t(nblk) << B0) & NM, B0 + nt)), T[(k + 1) & 1]);
+#pragma unroll
+      for (int i = 0; i < d; ++i) fb(s, blk + i, blk + i + d, T[k & 1]);
+    }
+  }
+}
+
+// layout C, L = 9 or 10: stage 8 (pairs r bit 0, skew by p9 when local) and stage 9 (L = 10)
+template <int L>
+__device__ __forceinline__ void ipassCg(S16 &s, const uint8_t *tabs) {
+  constexpr uint32_t NM = (1u << L) - 1;
+  Tab Ta, Tb;
+  tab_at(tabs, tlin(skew_idx(0, 8)), Ta);
+  tab_at(tabs, tlin(skew_idx((1u << 9) & NM, 8)), Tb);
+#pragma unroll
+  for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi, 4 * hi + 1, Ta);
+#pragma unroll
+  for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi + 2, 4 * hi + 3, Tb);
+  if constexpr (L == 10) {
+    tab_at(tabs, tlin(skew_idx(0, 9)), Ta);
+#pragma unroll
+    for (int hi = 0; hi < 4; ++hi) {
+      ib(s, 4 * hi, 4 * hi + 2, Ta);
+      ib(s, 4 * hi + 1, 4 * hi + 3, Ta);
+    }
+  }
+}
+
+template <int L>
+__device__ __forceinline__ void fpassCg(S16 &s, const uint8_t *tabs) {
+  constexpr uint32_t NM = (1u << L) - 1;
+  Tab Ta, Tb;
+  if constexpr (L == 10) {
+    tab_at(tabs, tlin(skew_idx(0, 9)), Ta);
+#pragma unroll
+    for (int hi = 0; hi < 4; ++hi) {
+      fb(s, 4 * hi, 4 * hi + 2, Ta);
+      fb(s, 4 * hi + 1, 4 * hi + 3, Ta);
+    }
+  }
+  tab_at(tabs, tlin(skew_idx(0, 8)), Ta);
+  tab_at(tabs, tlin(skew_idx((1u << 9) & NM, 8)), Tb);
+#pragma unroll
+  for (int hi = 0; hi < 4; ++hi) fb(s, 4 * hi, 4 * hi + 1, Ta);
+#pragma unroll
+  for (int hi = 0; hi < 4; ++hi) fb(s, 4 * hi + 2, 4 * hi + 3, Tb);
+}
+
+// formal derivative (poly_encoder.hpp:195-215), closed form, in layout X, in
+// place: registers in increasing order (register partners r | 2^t > r are
+// still original), lane partners read the other lanes' original register r
+template <Layout X, int L>
+__device__ __forceinline__ void derivative(S16 &s, uint32_t lane) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    uint32_t al = 0, ah = 0;
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      if (lane_pbit<X>(u) >= L) continue;  // an instance bit
+      const uint32_t m = ((lane >> u) & 1) ? 0u : 0xffffffffu;
+      al ^= from_upper(s.l[r], u) & m;
+      ah ^= from_upper(s.h[r], u) & m;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (reg_pbit<X>(t) < L && !(r & (1 << t))) {
+        al ^= s.l[r | (1 << t)];
+        ah ^= s.h[r | (1 << t)];
+      }
+    s.l[r] ^= al;
+    s.h[r] ^= ah;
+  }
+}
+
+template <int L>
+__global__ void __launch_bounds__(THREADS) reconstruct_gen(
+    const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
+    const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
+    uint8_t *__restrict__ out, uint64_t ostride, int nv, int k, uint32_t batch, DevTables t) {
+  constexpr int N = 1 << L;
+  constexpr uint32_t NM = N - 1;
+  constexpr int INST = 1024 >> L;          // codewords (x 4 columns) per wave
+  constexpr int TC = WAVES * 4 * INST;     // shard columns per tile
+  constexpr int CPR = TC * 2 / 16;         // 16-B chunks per received row
+  constexpr int CPT = N * CPR / THREADS;   // chunks per thread (8)
+  static_assert(N * CPR % THREADS == 0 && CPT == 8, "gather split");
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t *tabs = lds;
+  uint8_t *regions = lds + Tabs::kBytes;
+  const uint32_t tid0 = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid0 >> 6);
+  uint8_t *my = regions + wave * REG_BYTES;
+
+  Tabs::copy_image<THREADS>(tabs, t.timg, tid0);  // skews 0..1022 (index 0)
+  __syncthreads();
+
+  const uint64_t ncols = slen / 2;
+  const uint32_t tiles_pp = uint32_t((ncols + TC - 1) / TC);
+  const uint64_t total = uint64_t(tiles_pp) * batch;
+  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    uint32_t tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const uint32_t lane = tid & 63;
+    const uint64_t b = tile / tiles_pp;
+    const uint64_t col0 = (tile % tiles_pp) * TC;
+    const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
+    const uint8_t *pr = present + b * N;
+    const uint16_t *E = elog + b * N;
+    uint8_t *O = out + b * ostride;
+
+    // ---- gather + scale (decode_main:174-177): thread -> 8 consecutive
+    // 16-B chunks (8 columns = 2 groups each) of the tile's received rows
+    __syncthreads();  // previous tile's readers of the regions are done
+    {
+      const uint64_t avail = slen - 2 * col0;  // bytes of a row inside the tile
+      constexpr int RPT = CPR >= CPT ? 1 : CPT / CPR;  // rows per thread (2 for n = 1024)
+      constexpr int JPR = CPT / RPT;                   // chunks per row and thread
+#pragma unroll
+      for (int rr = 0; rr < RPT; ++rr) {
+        const uint32_t ch0 = tid * CPT + rr * JPR, v = ch0 / CPR;
+        const bool have = int(v) < nv && pr[v];
+        Tab T;  // absent rows: any table times zero
+        load_tab(t.mtab, mul_index(E[v]), T);
+#pragma unroll
+        for (int j = 0; j < JPR; ++j) {
+          const uint32_t c16 = ch0 % CPR + j;
+          uint32_t w[4] = {0, 0, 0, 0};
+          if (have) {
+            const uint8_t *src = SH + uint64_t(v) * sstride + 2 * col0 + 16 * c16;
+            if (16 * (c16 + 1) <= avail) {
+              const uint4 d = *reinterpret_cast<const uint4 *>(src);
+              w[0] = d.x; w[1] = d.y; w[2] = d.z; w[3] = d.w;
+            } else {
+              for (uint64_t e = 0; 16 * c16 + e < avail && e < 16; ++e)
+                w[e >> 2] |= uint32_t(src[e]) << (8 * (e & 3));
+            }
+          }
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {  // columns 8 c16 + 4 h2 .. + 3 = group 2 c16 + h2
+            const uint32_t g = 2 * c16 + h2, gw = g / INST, gi = g % INST;
+            uint32_t l = 0, h = 0;
+            const uint32_t a = w[2 * h2], c = w[2 * h2 + 1];
+            mul_acc(vperm(c, a, 0x07050301u), vperm(c, a, 0x06040200u), T, l, h);
+            *reinterpret_cast<uint2 *>(regions + gw * REG_BYTES + raddr((gi << L) | v)) =
+                make_uint2(l, h);
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- IFFT_n, derivative, FFT_n (back to layout A)
+    S16 s;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(posA(lane, r)));
+      s.l[r] = x.x;
+      s.h[r] = x.y;
+    }
+    // table addresses are recomputed from an opaque lane for every pass: the
+    // compiler would otherwise keep each pass's ~40 addresses live (spilled)
+    // from the IFFT to the mirrored FFT pass
+    auto lbA = [&] {
+      uint32_t l = lane;
+      asm volatile("" : "+v"(l));
+      return tlin((16 * l) & NM);
+    };
+    auto lbB = [&] {  // p8, p9 when local
+      uint32_t l = lane;
+      asm volatile("" : "+v"(l));
+      return tlin(((l >> 4) << 8) & NM);
+    };
+    ipassg<0, 4, L>(s, tabs, lbA());
+    __builtin_amdgcn_sched_barrier(0);
+    exchange<LA, LB>(s, my, lane);
+    if constexpr (L <= 8) {
+      ipassg<4, L - 4, L>(s, tabs, lbB());
+      __builtin_amdgcn_sched_barrier(0);
+      derivative<LB, L>(s, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      fpassg<4, L - 4, L>(s, tabs, lbB());
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      ipassg<4, 4, L>(s, tabs, lbB());
+      __builtin_amdgcn_sched_barrier(0);
+      exchange<LB, LC>(s, my, lane);
+      ipassCg<L>(s, tabs);
+      __builtin_amdgcn_sched_barrier(0);
+      derivative<LC, L>(s, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      fpassCg<L>(s, tabs);
+      __builtin_amdgcn_sched_barrier(0);
+      exchange<LC, LB>(s, my, lane);
+      fpassg<4, 4, L>(s, tabs, lbB());
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    exchange<LB, LA>(s, my, lane);
+    fpassg<0, 4, L>(s, tabs, lbA());
+#pragma unroll
+    for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(s.l[r]), "+v"(s.h[r]));  // finished here, not sunk past the fill
+
+    // ---- output tables E[y], y < k, into the regions
+    __syncthreads();  // every wave is done with its region
+    uint32_t ftid = tid;
+    asm volatile("" : "+v"(ftid));  // table loads not hoisted into the transform
+#pragma unroll
+    for (int it = 0; it < 5; ++it) {  // k * 5 <= 2560 16-B chunks
+      const uint32_t i = ftid + it * THREADS;
+      if (i < uint32_t(k) * 5)
+        *reinterpret_cast<uint4 *>(regions + OutTabs::addr(i / 5, i % 5)) =
+            reinterpret_cast<const uint4 *>(t.mtab + mul_index(E[i / 5]))[i % 5];
+    }
+    __syncthreads();
+
+    // ---- output (decode_main:185-188, reconstructSub:138-149): layout A,
+    // lane -> codeword gi, y = y0 .. y0 + 15
+#pragma unroll
+    for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(s.l[r]), "+v"(s.h[r]));  // mul_acc selects stay here
+    uint32_t olane = lane;
+    asm volatile("" : "+v"(olane));  // output addresses / shard re-reads not hoisted over the transform
+    const uint32_t gi = (16 * olane) >> L, y0 = (16 * olane) & NM;
+    if (y0 < uint32_t(k)) {
+      const uint64_t cbase = col0 + 4 * (uint64_t(wave) * INST + gi);
+      const bool full = cbase + 4 <= ncols;  // else the tile's last, partial group
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {  // 4 registers = 4 consecutive y at a time
+        uint32_t ol[4], oh[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 4 * q4 + q;
+          const uint32_t y = y0 + r;
+          const bool have = int(y) < nv && pr[y];
+          Tab T;
+          OutTabs::load(regions, y, T);
+          uint32_t ml = 0, mh = 0;
+          mul_acc(s.l[r], s.h[r], T, ml, mh);
+          uint32_t a = 0, c = 0;
+          const uint8_t *row = SH + uint64_t(have ? y : 0u) * sstride + 2 * cbase;
+          if (full) {
+            const uint2 d = *reinterpret_cast<const uint2 *>(row);
+            a = d.x;
+            c = d.y;
+          } else if (have && cbase < ncols) {
+            for (uint64_t e = 0; e < 2 * (ncols - cbase); ++e) {
+              if (e < 4) a |= uint32_t(row[e]) << (8 * e);
+              else c |= uint32_t(row[e]) << (8 * (e - 4));
+            }
+          }
+          oh[q] = have ? vperm(c, a, 0x06040200u) : mh;
+          ol[q] = have ? vperm(c, a, 0x07050301u) : ml;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {  // column c: 4 consecutive y -> 8 bytes BE
+          const uint64_t col = cbase + c;
+          if (col >= ncols) break;
+          const uint32_t w0 = vperm(ol[0], oh[0], 0x0c0c0400u + 0x0101u * c) |
+                              (vperm(ol[1], oh[1], 0x0c0c0400u + 0x0101u * c) << 16);
+          const uint32_t w1 = vperm(ol[2], oh[2], 0x0c0c0400u + 0x0101u * c) |
+                              (vperm(ol[3], oh[3], 0x0c0c0400u + 0x0101u * c) << 16);
+          *reinterpret_cast<uint2 *>(O + (col * uint64_t(k) + y0 + 4 * q4) * 2) = make_uint2(w0, w1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+}
+
+template <int L>
+hipError_t launch_l(const CodeParams &p, const DevTables &t, const uint8_t *d_shards, size_t slen,
+                    size_t sstride, const uint8_t *d_present, const uint16_t *d_err_log,
+                    size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&reconstruct_gen<L>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e != hipSuccess) return e;
+  }
+  constexpr int TC = WAVES * 4 * (1024 >> L);
+  const size_t tiles = (slen / 2 + TC - 1) / TC * batch;
+  const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
+  hipLaunchKernelGGL(reconstruct_gen<L>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
+                     uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out,
+                     uint64_t(ostride), int(p.nv), int(p.k), uint32_t(batch), t);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool decgen_applicable(const CodeParams &p) {
+  return p.n >= 64 && p.n <= 1024 && p.k >= 16 && p.k <= 512 && p.k % 16 == 0 && p.k < p.n;
+}
+
+hipError_t launch_reconstruct_gen(const CodeParams &p, const DevTables &t,
+                                  const uint8_t *d_shards, size_t slen, size_t sstride,
+                                  const uint8_t *d_present, const uint16_t *d_err_log,
+                                  size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
+  switch (p.n) {
+    case 64: return launch_l<6>(p, t, d_shards, slen, sstride, d_present, d_err_log, batch, d_out, ostride, s);
+    case 128: return launch_l<7>(p, t, d_shards, slen, sstride, d_present, d_err_log, batch, d_out, ostride, s);
+    case 256: return launch_l<8>(p, t, d_shards, slen, sstride, d_present, d_err_log, batch, d_out, ostride, s);
+    case 512: return launch_l<9>(p, t, d_shards, slen, sstride, d_present, d_err_log, batch, d_out, ostride, s);
+    default: return launch_l<10>(p, t, d_shards, slen, sstride, d_present, d_err_log, batch, d_out, ostride, s);
+  }
+}
+
+}  // namespace ecamd

@@ -370,6 +370,10 @@ hipError_t launch_reconstruct(const CodeParams &p, const DevTables &t, const uin
       (batch == 1 || ostride % 16 == 0))
     return launch_reconstruct_n4096(p, t, d_shards, slen, sstride, d_present, d_err_log, batch,
                                     d_out, ostride, s);
+  if (aligned && decgen_applicable(p) && reinterpret_cast<uintptr_t>(d_out) % 16 == 0 &&
+      (batch == 1 || ostride % 16 == 0))
+    return launch_reconstruct_gen(p, t, d_shards, slen, sstride, d_present, d_err_log, batch,
+                                  d_out, ostride, s);
   const int G = groups_for(p.n);
   const size_t tiles = (slen / 2 + 4 * G - 1) / (4 * G);
   const bool lds = p.n <= uint32_t(kLdsSlots);

@@ -80,4 +80,11 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
                                     const uint8_t *d_present, const uint16_t *d_err_log,
                                     size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s);
 
+// register-blocked reconstruct for 64 <= n <= 1024, 16 <= k <= 512 (dec_gen.hip)
+bool decgen_applicable(const CodeParams &p);
+hipError_t launch_reconstruct_gen(const CodeParams &p, const DevTables &t,
+                                  const uint8_t *d_shards, size_t slen, size_t sstride,
+                                  const uint8_t *d_present, const uint16_t *d_err_log,
+                                  size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s);
+
 }  // namespace ecamd
