@@ -239,7 +239,9 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         } else {
 #pragma unroll
           for (int q = 0; q < 16; ++q) w[q] = 0;
-          for (uint64_t e = 0; e < avail; ++e) w[e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
+          #pragma unroll
+          for (int e = 0; e < 64; ++e)  // constant trip count: w stays in registers
+            if (uint64_t(e) < avail) w[e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
         }
         Tab T;
         if (DEC_ABL & 2) Tabs::load(tabs, v & 1023, T);

@@ -1,5 +1,7 @@
 // dec_n4096.hip — reconstruct specialised for n = 4096, k = 1024
-// (n_validators 3070..4096; BASELINE config 4).
+// (n_validators 3070..4096; BASELINE config 4), instantiated as well for
+// n = 2048 (two halves, stage 10 only across them) and for k = 256 / 512 (only
+// the outputs y < k of the final FFT_1024 are written): n_validators 1025..4096.
 //
 // decode_main (poly_encoder.hpp:164-189) at n = 4096 per codeword (shard
 // column): IFFT_4096 of the locator-scaled received word, formal derivative,
@@ -25,8 +27,6 @@ namespace ecamd {
 namespace {
 
 using namespace tf;
-constexpr int N = 4096;
-constexpr int K = 1024;
 #ifndef DEC4_WAVES
 #define DEC4_WAVES 8
 #endif
@@ -60,6 +60,8 @@ __device__ __forceinline__ uint32_t from_upper(uint32_t x, int b) {
 
 }  // namespace
 
+// NQ = n / 1024 quarters (2 or 4); K = k (256, 512 or 1024)
+template <int NQ>
 __global__ void __launch_bounds__(THREADS)
 #if DEC4_WAVES == 4
 __attribute__((amdgpu_waves_per_eu(1, 1)))
@@ -67,7 +69,9 @@ __attribute__((amdgpu_waves_per_eu(1, 1)))
 reconstruct_n4096(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
-    uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t batch, DevTables t) {
+    uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t K, uint32_t batch,
+    DevTables t) {
+  constexpr int N = 1024 * NQ;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
   uint8_t *regions = lds + Tabs::kBytes;
@@ -87,7 +91,7 @@ reconstruct_n4096(
     const uint8_t *pr = present + b * N;
     const uint16_t *E = elog + b * N;
     uint8_t *O = out + b * ostride;
-    S16 Q[4];
+    S16 Q[NQ];
 
     // ---- IFFT quarters 3, 2, 1, 0 (quarter 0's tables stay for the FFT); a
     // lambda called per quarter so every Q[] index is a constant (a loop the
@@ -123,7 +127,9 @@ reconstruct_n4096(
           } else {
 #pragma unroll
             for (int j = 0; j < 16; ++j) w[j] = 0;
-            for (uint64_t e = 0; e < avail; ++e) w[e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
+            #pragma unroll
+            for (int e = 0; e < 64; ++e)  // constant trip count: w stays in registers
+              if (uint64_t(e) < avail) w[e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
           }
           Tab T;
           load_tab(t.mtab, mul_index(E[v]), T);
@@ -150,35 +156,39 @@ reconstruct_n4096(
       ifft1024(Qq, tabs, my, lane);  // -> layout C
       __builtin_amdgcn_sched_barrier(0);
     };
-    quarter(Q[3], 3);
-    quarter(Q[2], 2);
+    if constexpr (NQ == 4) {
+      quarter(Q[NQ - 1], 3);
+      quarter(Q[NQ - 2], 2);
+    }
     quarter(Q[1], 1);
     quarter(Q[0], 0);
 
     // ---- IFFT stages 10 (skews 1023 / 3071) and 11 (skew 2047) across quarters
     Tab T10a, T10b, T11;
     load_tab(t.mtab, t.skews[1023], T10a);
-    load_tab(t.mtab, t.skews[3071], T10b);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       Q[1].l[r] ^= Q[0].l[r];
       Q[1].h[r] ^= Q[0].h[r];
       mul_acc(Q[1].l[r], Q[1].h[r], T10a, Q[0].l[r], Q[0].h[r]);
     }
-    load_tab(t.mtab, t.skews[2047], T11);
+    if constexpr (NQ == 4) {
+      load_tab(t.mtab, t.skews[3071], T10b);
+      load_tab(t.mtab, t.skews[2047], T11);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      Q[3].l[r] ^= Q[2].l[r];
-      Q[3].h[r] ^= Q[2].h[r];
-      mul_acc(Q[3].l[r], Q[3].h[r], T10b, Q[2].l[r], Q[2].h[r]);
-    }
+      for (int r = 0; r < 16; ++r) {
+        Q[NQ - 1].l[r] ^= Q[NQ - 2].l[r];
+        Q[NQ - 1].h[r] ^= Q[NQ - 2].h[r];
+        mul_acc(Q[NQ - 1].l[r], Q[NQ - 1].h[r], T10b, Q[NQ - 2].l[r], Q[NQ - 2].h[r]);
+      }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
+      for (int r = 0; r < 16; ++r) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        Q[q + 2].l[r] ^= Q[q].l[r];
-        Q[q + 2].h[r] ^= Q[q].h[r];
-        mul_acc(Q[q + 2].l[r], Q[q + 2].h[r], T11, Q[q].l[r], Q[q].h[r]);
+        for (int q = 0; q < 2; ++q) {
+          Q[q + NQ - 2].l[r] ^= Q[q].l[r];
+          Q[q + NQ - 2].h[r] ^= Q[q].h[r];
+          mul_acc(Q[q + NQ - 2].l[r], Q[q + NQ - 2].h[r], T11, Q[q].l[r], Q[q].h[r]);
+        }
       }
     }
 
@@ -187,7 +197,7 @@ reconstruct_n4096(
     // still original when (q, r) is processed; lane partners read the other
     // lanes' original (q, r).  Bits: lane = p0..p5, r = (p8, p9, p6, p7), q = (p10, p11).
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NQ; ++q) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         uint32_t al = 0, ah = 0;
@@ -205,7 +215,7 @@ reconstruct_n4096(
           }
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb)
-          if (!(q & (1 << qb))) {
+          if ((1 << qb) < NQ && !(q & (1 << qb))) {
             al ^= Q[q | (1 << qb)].l[r];
             ah ^= Q[q | (1 << qb)].h[r];
           }
@@ -215,15 +225,19 @@ reconstruct_n4096(
     }
 
     // ---- FFT stage 11 (keep v < 2048) and stage 10 (keep v < 1024): a ^= b * s
+    if constexpr (NQ == 4) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      mul_acc(Q[2].l[r], Q[2].h[r], T11, Q[0].l[r], Q[0].h[r]);
-      mul_acc(Q[3].l[r], Q[3].h[r], T11, Q[1].l[r], Q[1].h[r]);
+      for (int r = 0; r < 16; ++r) {
+        mul_acc(Q[NQ - 2].l[r], Q[NQ - 2].h[r], T11, Q[0].l[r], Q[0].h[r]);
+        mul_acc(Q[NQ - 1].l[r], Q[NQ - 1].h[r], T11, Q[1].l[r], Q[1].h[r]);
+      }
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) mul_acc(Q[1].l[r], Q[1].h[r], T10a, Q[0].l[r], Q[0].h[r]);
     // ---- FFT_1024, index 0, on quarter 0 (tables of quarter 0 still resident)
     fft1024(Q[0], tabs, my, lane);  // -> layout A: y = 16 lane + r
+#pragma unroll
+    for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(Q[0].l[r]), "+v"(Q[0].h[r]));  // not sunk past the table gather
 
     // ---- output (decode_main:185-188, reconstructSub:138-149): erased y < k
     // scaled by E[y] (tables now in LDS), present y copied from the shard
@@ -231,50 +245,54 @@ reconstruct_n4096(
     Tabs::gather<THREADS>(tabs, t.mtab, [&](uint32_t y) { return mul_index(E[y]); }, tid);
     lds_barrier();
     const uint64_t cbase = col0 + 4 * wave;
-    uint32_t ol[16], oh[16];
+    if (16 * lane < K) {  // k < 1024: the other lanes' y are not read
+      uint32_t ol[16], oh[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const uint32_t y = 16 * lane + r;
-      ol[r] = oh[r] = 0;
-      if (int(y) < nv && pr[y]) {
-        const uint8_t *row = SH + uint64_t(y) * sstride + 2 * cbase;
-        uint32_t a = 0, c = 0;
-        if (cbase + 4 <= ncols) {
-          const uint2 d = *reinterpret_cast<const uint2 *>(row);
-          a = d.x;
-          c = d.y;
-        } else {
-          for (uint64_t e = 0; e < 2 * (ncols > cbase ? ncols - cbase : 0); ++e) {
-            if (e < 4) a |= uint32_t(row[e]) << (8 * e);
-            else c |= uint32_t(row[e]) << (8 * (e - 4));
+      for (int r = 0; r < 16; ++r) {
+        const uint32_t y = 16 * lane + r;
+        ol[r] = oh[r] = 0;
+        if (int(y) < nv && pr[y]) {
+          const uint8_t *row = SH + uint64_t(y) * sstride + 2 * cbase;
+          uint32_t a = 0, c = 0;
+          if (cbase + 4 <= ncols) {
+            const uint2 d = *reinterpret_cast<const uint2 *>(row);
+            a = d.x;
+            c = d.y;
+          } else {
+            for (uint64_t e = 0; e < 2 * (ncols > cbase ? ncols - cbase : 0); ++e) {
+              if (e < 4) a |= uint32_t(row[e]) << (8 * e);
+              else c |= uint32_t(row[e]) << (8 * (e - 4));
+            }
           }
+          oh[r] = vperm(c, a, 0x06040200u);
+          ol[r] = vperm(c, a, 0x07050301u);
+        } else {
+          Tab T;
+          Tabs::load(tabs, y, T);
+          mul_acc(Q[0].l[r], Q[0].h[r], T, ol[r], oh[r]);
         }
-        oh[r] = vperm(c, a, 0x06040200u);
-        ol[r] = vperm(c, a, 0x07050301u);
-      } else {
-        Tab T;
-        Tabs::load(tabs, y, T);
-        mul_acc(Q[0].l[r], Q[0].h[r], T, ol[r], oh[r]);
       }
-    }
-    // column c: y = 16 lane .. 16 lane + 15 -> 32 contiguous bytes (BE symbols)
+      // column c: y = 16 lane .. 16 lane + 15 -> 32 contiguous bytes (BE symbols)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const uint64_t col = cbase + c;
-      if (col >= ncols) break;
-      uint32_t wd[8];
+      for (int c = 0; c < 4; ++c) {
+        const uint64_t col = cbase + c;
+        if (col >= ncols) break;
+        uint32_t wd[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        wd[j] = vperm(ol[2 * j], oh[2 * j], 0x0c0c0400u + 0x0101u * c) |
-                (vperm(ol[2 * j + 1], oh[2 * j + 1], 0x0c0c0400u + 0x0101u * c) << 16);
-      uint8_t *dst = O + (col * K + 16 * lane) * 2;
-      reinterpret_cast<uint4 *>(dst)[0] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
-      reinterpret_cast<uint4 *>(dst)[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);
+        for (int j = 0; j < 8; ++j)
+          wd[j] = vperm(ol[2 * j], oh[2 * j], 0x0c0c0400u + 0x0101u * c) |
+                  (vperm(ol[2 * j + 1], oh[2 * j + 1], 0x0c0c0400u + 0x0101u * c) << 16);
+        uint8_t *dst = O + (col * K + 16 * lane) * 2;
+        reinterpret_cast<uint4 *>(dst)[0] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+        reinterpret_cast<uint4 *>(dst)[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);
+      }
     }
   }
 }
 
-bool n4096_applicable(const CodeParams &p) { return p.n == 4096 && p.k == 1024; }
+bool n4096_applicable(const CodeParams &p) {
+  return (p.n == 4096 || p.n == 2048) && p.k >= 256 && p.k <= 1024;
+}
 
 hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
                                     const uint8_t *d_shards, size_t slen, size_t sstride,
@@ -286,15 +304,23 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&reconstruct_n4096),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&reconstruct_n4096<4>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&reconstruct_n4096<2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return e;
   }
   const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
-  hipLaunchKernelGGL(reconstruct_n4096, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
-                     uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out,
-                     uint64_t(ostride), int(p.nv), uint32_t(batch), t);
+  if (p.n == 4096)
+    hipLaunchKernelGGL(reconstruct_n4096<4>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
+                       uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out,
+                       uint64_t(ostride), int(p.nv), uint32_t(p.k), uint32_t(batch), t);
+  else
+    hipLaunchKernelGGL(reconstruct_n4096<2>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
+                       uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out,
+                       uint64_t(ostride), int(p.nv), uint32_t(p.k), uint32_t(batch), t);
   return hipGetLastError();
 }
 

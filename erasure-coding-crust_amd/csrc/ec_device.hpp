@@ -117,13 +117,18 @@ struct LdsTabs {
                                                     uint32_t tid) {
     constexpr int kChunks = kBytes / 16;
     static_assert(kChunks % THREADS == 0, "whole chunks per thread");
-    uint4 v[kChunks / THREADS];
+    uint32_t v[kChunks / THREADS][4];  // scalars, not uint4: an aggregate copy would stay in scratch
+#pragma unroll
+    for (int k = 0; k < kChunks / THREADS; ++k) {
+      const uint4 x = reinterpret_cast<const uint4 *>(img)[tid + k * THREADS];
+      v[k][0] = x.x;
+      v[k][1] = x.y;
+      v[k][2] = x.z;
+      v[k][3] = x.w;
+    }
 #pragma unroll
     for (int k = 0; k < kChunks / THREADS; ++k)
-      v[k] = reinterpret_cast<const uint4 *>(img)[tid + k * THREADS];
-#pragma unroll
-    for (int k = 0; k < kChunks / THREADS; ++k)
-      reinterpret_cast<uint4 *>(base)[tid + k * THREADS] = v[k];
+      reinterpret_cast<uint4 *>(base)[tid + k * THREADS] = make_uint4(v[k][0], v[k][1], v[k][2], v[k][3]);
   }
   // the same copy by LDS-DMA (global_load_lds_dwordx4): no VGPRs, completes in
   // the background; the caller retires it (s_waitcnt vmcnt(0)) before the
@@ -148,22 +153,24 @@ struct LdsTabs {
                                                 uint32_t tid) {
     constexpr int kChunks = ENTRIES * 5;
     constexpr int kPer = (kChunks + THREADS - 1) / THREADS;
+    constexpr bool kExact = kChunks % THREADS == 0;  // no bounds test (keeps v[] in registers)
     uint32_t c[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint32_t i = tid + k * THREADS;
-      c[k] = i < uint32_t(kChunks) ? src(i / 5) : 0u;
+      c[k] = (kExact || i < uint32_t(kChunks)) ? src(i / 5) : 0u;
     }
     uint4 v[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint32_t i = tid + k * THREADS;
-      if (i < uint32_t(kChunks)) v[k] = reinterpret_cast<const uint4 *>(mtab + c[k])[i % 5];
+      v[k] = make_uint4(0, 0, 0, 0);
+      if (kExact || i < uint32_t(kChunks)) v[k] = reinterpret_cast<const uint4 *>(mtab + c[k])[i % 5];
     }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint32_t i = tid + k * THREADS;
-      if (i < uint32_t(kChunks)) *reinterpret_cast<uint4 *>(base + addr(i / 5, i % 5)) = v[k];
+      if (kExact || i < uint32_t(kChunks)) *reinterpret_cast<uint4 *>(base + addr(i / 5, i % 5)) = v[k];
     }
   }
   // cooperative fill: entry i <- mtab[src(i)]

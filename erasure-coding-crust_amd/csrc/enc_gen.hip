@@ -1,6 +1,7 @@
-// enc_gen.hip — register-blocked encode for k = 2^M, M = 5..7 (k = 32, 64,
-// 128) and n <= 1024: n_validators ~96..765, which includes today's Polkadot
-// validator counts (k = 128, n = 1024 for 512..765 validators).
+// enc_gen.hip — register-blocked encode for k = 2^M, M = 5..9 (k = 32 .. 512)
+// and n <= 4096: n_validators ~96..3069 outside the k = 256 / n = 1024 and
+// k = 1024 / n = 4096 kernels; this includes today's Polkadot validator counts
+// (k = 128, n = 1024 for 512..765 validators) and n = 2048 / 4096 with k = 256 / 512.
 //
 // The 1024 positions a wave holds (tf1024.hpp: 64 lanes x 16 registers, 4
 // pieces per byte-planar register) are read as 1024 / k independent k-point
@@ -11,10 +12,12 @@
 //   FFT_k at each coset s = k, 2k, .. < n: pass B (stages M-1..4), B -> A
 //             exchange, pass A (stages 3..0): ends in layout A = shard rows.
 // Stage index arithmetic only sees the local bits (pos & (k-1)); instance bits
-// ride along as extra register / lane bits.  All n - 1 <= 1023 skews of an
-// n <= 1024 code are one LDS table image (set 0); a coset's tables are that
-// image at offset s, folded into the linear table address (tlin).  In layout B
-// every table index is wave-uniform.
+// ride along as extra register / lane bits.  k = 512 adds stage 8, done in
+// layout C (IFFT: A -> B -> C, coset FFT: C -> B -> A).  Skews 1024q .. 1024q +
+// 1023 are LDS table image q; a coset s uses image s / 1024 at offset s % 1024,
+// folded into the linear table address (tlin): n <= 1024 needs image 0 only,
+// n = 2048 / 4096 reload the image when s crosses a multiple of 1024 (and
+// image 0 again for the next tile's IFFT).
 //
 // Shard rows: per coset, k rows x 32 * 1024 / k pieces (64 KB) are staged in the
 // waves' own regions (row v of wave w: 8 * 1024 / k bytes) and stored as 16-B
@@ -83,6 +86,28 @@ __device__ __forceinline__ void fpassg(S16 &s, const uint8_t *tabs, uint32_t lb)
   }
 }
 
+// k = 512: pass B's lane part is p8 (lane bit 4); p9 is an instance bit
+__device__ __forceinline__ uint32_t lbB(uint32_t lane) {
+  asm volatile("" : "+v"(lane));
+  return tlin(((lane >> 4) & 1) << 8);
+}
+
+// k = 512, layout C: stage 8 (register bit 0); its skew index 255 (+ offset)
+// is uniform since p9 is an instance bit
+__device__ __forceinline__ void ipassC9(S16 &s, const uint8_t *tabs, uint32_t lo) {
+  Tab T;
+  tab_at(tabs, lo ^ tlin(skew_idx(0, 8)), T);
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) ib(s, r, r + 1, T);
+}
+
+__device__ __forceinline__ void fpassC9(S16 &s, const uint8_t *tabs, uint32_t lo) {
+  Tab T;
+  tab_at(tabs, lo ^ tlin(skew_idx(0, 8)), T);
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) fb(s, r, r + 1, T);
+}
+
 // layout A rows of the wave -> own region: row local, instance i -> 8 B at
 // row * ROWB + 8 i
 template <int M>
@@ -124,8 +149,10 @@ __device__ __forceinline__ void store_rows(const uint8_t *regions, uint8_t *SH, 
       }
     } else {
       const uint32_t wd[4] = {val.x, val.y, val.z, val.w};
-      for (uint64_t e = 0; e < npieces - p; ++e)
-        *reinterpret_cast<uint16_t *>(dst + 2 * e) = uint16_t(wd[e >> 1] >> (16 * (e & 1)));
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (p + e < npieces)
+          *reinterpret_cast<uint16_t *>(dst + 2 * e) = uint16_t(wd[e >> 1] >> (16 * (e & 1)));
     }
   }
 }
@@ -142,6 +169,12 @@ __global__ void __launch_bounds__(THREADS)
   const uint32_t tid0 = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid0 >> 6);
   uint8_t *my = regions + wave * REG_BYTES;
 
+  int img = 0;  // table image in LDS: skews 1024 img .. + 1022
+  const auto load_image = [&](int q) {
+    lds_barrier();  // every wave is done with the current tables
+    Tabs::copy_image<THREADS>(tabs, t.timg + q * kTabImageBytes, tid0);
+    lds_barrier();
+  };
   Tabs::copy_image<THREADS>(tabs, t.timg, tid0);  // skews 0..1022: every coset of n <= 1024
   __syncthreads();
 
@@ -174,8 +207,9 @@ __global__ void __launch_bounds__(THREADS)
         } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j) D[u][j] = 0;
-          for (uint64_t e = off; e < plen && e < off + 32; ++e)
-            D[u][(e - off) >> 2] |= uint32_t(P[e]) << (8 * ((e - off) & 3));
+#pragma unroll
+          for (int e = 0; e < 32; ++e)  // constant trip count: D stays in registers
+            if (off + e < plen) D[u][e >> 2] |= uint32_t(P[off + e]) << (8 * (e & 3));
         }
       }
 #pragma unroll
@@ -197,19 +231,39 @@ __global__ void __launch_bounds__(THREADS)
     lds_barrier();
 
     // ---- IFFT_k (index 0): pass A, exchange, pass B -> layout B
+    if (img != 0) {  // the previous tile ended on a higher image
+      load_image(0);
+      img = 0;
+    }
     const uint32_t lbA = tlin((16 * lane) & (Gm::K - 1));
     ipassg<0, (M < 4 ? M : 4), M>(s, tabs, lbA);
     exchange<LA, LB>(s, my, lane);
-    ipassg<4, M - 4, M>(s, tabs, 0);
+    if constexpr (M <= 8) {
+      ipassg<4, M - 4, M>(s, tabs, 0);
+    } else {
+      ipassg<4, 4, M>(s, tabs, lbB(lane));
+      exchange<LB, LC>(s, my, lane);
+      ipassC9(s, tabs, 0);
+    }
     const S16 coef = s;
 
     // ---- FFT_k at each coset shift (encodeLow, poly_encoder.hpp:229-237)
     for (int sh = int(Gm::K); sh < n && sh < nv; sh += int(Gm::K)) {
+      if ((sh >> 10) != img) {  // every wave is past the last barrier of the previous coset
+        img = sh >> 10;
+        load_image(img);
+      }
       s = coef;
 #pragma unroll
       for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(s.l[r]), "+v"(s.h[r]));
-      const uint32_t lo = tlin(uint32_t(sh));  // tables at offset sh (disjoint bits)
-      fpassg<4, M - 4, M>(s, tabs, lo);
+      const uint32_t lo = tlin(uint32_t(sh) & 1023u);  // tables at offset sh (disjoint bits)
+      if constexpr (M <= 8) {
+        fpassg<4, M - 4, M>(s, tabs, lo);
+      } else {
+        fpassC9(s, tabs, lo);
+        exchange<LC, LB>(s, my, lane);
+        fpassg<4, 4, M>(s, tabs, lbB(lane) ^ lo);
+      }
       exchange<LB, LA>(s, my, lane);
       fpassg<0, (M < 4 ? M : 4), M>(s, tabs, tlin((16 * lane) & (Gm::K - 1)) ^ lo);
       lds_barrier();  // all waves done with their regions (exchange, previous stores)
@@ -247,7 +301,7 @@ hipError_t launch_m(const CodeParams &p, const DevTables &t, const uint8_t *d_pa
 }  // namespace
 
 bool encgen_applicable(const CodeParams &p) {
-  return (p.k == 32 || p.k == 64 || p.k == 128) && p.n <= 1024 && p.n >= 2 * p.k;
+  return p.k >= 32 && p.k <= 512 && (p.k & (p.k - 1)) == 0 && p.n <= 4096 && p.n >= 2 * p.k;
 }
 
 hipError_t launch_encode_gen(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
@@ -256,7 +310,9 @@ hipError_t launch_encode_gen(const CodeParams &p, const DevTables &t, const uint
   switch (p.k) {
     case 32: return launch_m<5>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
     case 64: return launch_m<6>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
-    default: return launch_m<7>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
+    case 128: return launch_m<7>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
+    case 256: return launch_m<8>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
+    default: return launch_m<9>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
   }
 }
 

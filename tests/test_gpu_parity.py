@@ -93,8 +93,8 @@ def test_golden_vectors(golden_vectors):
 
 # ---------------------------------------------------------------- random sweep vs oracle
 @pytest.mark.parametrize("nv", [2, 3, 5, 6, 7, 9, 16, 33, 46, 64, 65, 100, 128, 129, 200, 255, 256,
-                                257, 300, 384, 512, 600, 700, 765, 1000, 1024, 2048, 3070, 3500,
-                                4096])
+                                257, 300, 384, 512, 600, 700, 765, 1000, 1024, 1025, 1366, 1367,
+                                2048, 2049, 3000, 3069, 3070, 3500, 4096])
 def test_random_vs_oracle(oracle, nv):
     rng = np.random.default_rng(nv)
     n, k, thr = E.code_params(nv)
@@ -164,7 +164,11 @@ def _batch_case(nv, plen, batch, cnt_key="threshold", seed0=0, pad=0):
     # 64 <= n <= 1024, 16 <= k <= 512 register-blocked reconstruct (every n / k
     # shape): several tiles, partial last tile, 16/64-byte pitches
     (46, 70001, 2, 64), (65, 9999, 3, 16), (129, 33333, 2, 16), (257, 100001, 2, 64),
-    (512, 200001, 2, 64), (765, 300001, 2, 64), (600, 1, 2, 16)])
+    (512, 200001, 2, 64), (765, 300001, 2, 64), (600, 1, 2, 16),
+    # n = 2048 / 4096 with k = 256 / 512: encode with per-coset table images,
+    # reconstruct by halves / quarters with k < 1024 outputs
+    (1025, 5000, 3, 64), (1500, 200001, 2, 64), (2048, 100001, 2, 16), (2500, 300001, 2, 64),
+    (3069, 4097, 2, 16)])
 def test_batch_vs_oracle(oracle, nv, plen, batch, pad):
     pay, pres, sh, el, out = _batch_case(nv, plen, batch, pad=pad)
     n, k, _ = E.code_params(nv)
