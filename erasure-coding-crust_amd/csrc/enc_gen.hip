@@ -129,7 +129,7 @@ __device__ __forceinline__ void store_rows(const uint8_t *regions, uint8_t *SH, 
   constexpr int CPR = CPW * WAVES;        // chunks per row
   constexpr int ITER = Gm::K * CPR / THREADS;
   static_assert(Gm::K * CPR % THREADS == 0, "whole iterations");
-  const bool wide = (sstride & 15) == 0;
+  const bool wide = ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0;  // 16-B aligned rows
 #pragma unroll 4
   for (int it = 0; it < ITER; ++it) {
     const uint32_t ch = uint32_t(it) * THREADS + tid;

@@ -59,7 +59,7 @@ __device__ __forceinline__ void store_half(const uint8_t *regions, uint8_t *SH, 
                                            uint64_t npieces, uint32_t wave, uint32_t lane) {
   const uint32_t c = lane & 7;
   const uint64_t p = piece0 + 8 * c;
-  const bool wide = (sstride & 15) == 0;
+  const bool wide = ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0;  // 16-B aligned rows
   const uint8_t *src = regions + c * REG_BYTES;
 #pragma unroll 2
   for (int it = 0; it < 512 / (8 * WAVES); ++it) {

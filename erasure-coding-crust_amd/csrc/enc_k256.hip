@@ -421,7 +421,7 @@ __device__ __forceinline__ void store_rows16(const uint8_t *stg, uint8_t *SH, ui
                                              uint64_t npieces, uint32_t wave, uint32_t lane) {
   const uint32_t c = lane & 15;
   const uint64_t p = piece0 + 8 * c;
-  const bool wide = (sstride & 15) == 0;
+  const bool wide = ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0;  // 16-B aligned rows
 #pragma unroll
   for (int it = 0; it < 256 / (4 * WAVES); ++it) {
     const uint32_t v = uint32_t(it) * 4 * WAVES + wave * 4 + (lane >> 4);
@@ -470,7 +470,7 @@ __device__ __forceinline__ void store_own(const uint8_t *xbase, uint8_t *SH, uin
   asm volatile("" : "+v"(lane));  // recomputed here, not kept live across the FFTs
   const uint32_t c = lane & 15;
   const uint64_t p = piece0 + 8 * c;
-  const bool wide = (sstride & 15) == 0;
+  const bool wide = ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0;  // 16-B aligned rows
   const uint8_t *src = xbase + c * XCH_BYTES;
 #pragma unroll
   for (int it = 0; it < 256 / (4 * WAVES); ++it) {
