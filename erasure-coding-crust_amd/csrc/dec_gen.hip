@@ -26,9 +26,9 @@ namespace {
 using namespace tf;
 constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
-using OutTabs = LdsTabs<512>;  // E[y], y < k <= 512, in the regions
-constexpr int LDS_BYTES = Tabs::kBytes + WAVES * REG_BYTES;
-static_assert(LDS_BYTES <= 160 * 1024 && OutTabs::kBytes <= WAVES * REG_BYTES, "LDS budget");
+using OutTabs = LdsTabs<128>;  // E[y], y < k <= 128, own area: filled once per payload
+constexpr int LDS_BYTES = Tabs::kBytes + WAVES * REG_BYTES + OutTabs::kBytes;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 
 __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ? 0u : c; }
 
@@ -190,16 +190,27 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
   uint8_t *regions = lds + Tabs::kBytes;
+  uint8_t *outtabs = regions + WAVES * REG_BYTES;
   const uint32_t tid0 = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid0 >> 6);
   uint8_t *my = regions + wave * REG_BYTES;
 
   Tabs::copy_image<THREADS>(tabs, t.timg, tid0);  // skews 0..1022 (index 0)
   __syncthreads();
 
+  // a contiguous range of tiles per workgroup, so consecutive tiles share a
+  // payload and its locator state: the gather's per-row tables (registers)
+  // and the output tables E[y] (LDS) are loaded once per payload, not per tile
+  constexpr int RPT = CPR >= CPT ? 1 : CPT / CPR;  // received rows per thread (2 for n = 1024)
+  constexpr int JPR = CPT / RPT;                   // chunks per row and thread
   const uint64_t ncols = slen / 2;
   const uint32_t tiles_pp = uint32_t((ncols + TC - 1) / TC);
   const uint64_t total = uint64_t(tiles_pp) * batch;
-  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+  const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
+  const uint64_t tile_end = per * (blockIdx.x + 1) < total ? per * (blockIdx.x + 1) : total;
+  uint64_t cur_b = ~0ull;
+  Tab RT[RPT];  // E[v] tables of this thread's received rows
+  bool rhave[RPT];
+  for (uint64_t tile = per * blockIdx.x; tile < tile_end; ++tile) {
     uint32_t tid = tid0;
     asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63;
@@ -210,19 +221,33 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
     const uint16_t *E = elog + b * N;
     uint8_t *O = out + b * ostride;
 
+    __syncthreads();  // previous tile's readers of the regions / output tables are done
+    if (b != cur_b) {  // new payload (uniform): its row tables and output tables
+      cur_b = b;
+#pragma unroll
+      for (int rr = 0; rr < RPT; ++rr) {
+        const uint32_t v = (tid * CPT + rr * JPR) / CPR;
+        rhave[rr] = int(v) < nv && pr[v];
+        load_tab(t.mtab, mul_index(E[v]), RT[rr]);  // absent rows: any table times zero
+      }
+#pragma unroll
+      for (int it = 0; it < (128 * 5 + THREADS - 1) / THREADS; ++it) {  // k * 5 <= 640 chunks
+        const uint32_t i = tid + it * THREADS;
+        if (i < uint32_t(k) * 5)
+          *reinterpret_cast<uint4 *>(outtabs + OutTabs::addr(i / 5, i % 5)) =
+              reinterpret_cast<const uint4 *>(t.mtab + mul_index(E[i / 5]))[i % 5];
+      }
+    }
+
     // ---- gather + scale (decode_main:174-177): thread -> 8 consecutive
     // 16-B chunks (8 columns = 2 groups each) of the tile's received rows
-    __syncthreads();  // previous tile's readers of the regions are done
     {
       const uint64_t avail = slen - 2 * col0;  // bytes of a row inside the tile
-      constexpr int RPT = CPR >= CPT ? 1 : CPT / CPR;  // rows per thread (2 for n = 1024)
-      constexpr int JPR = CPT / RPT;                   // chunks per row and thread
 #pragma unroll
       for (int rr = 0; rr < RPT; ++rr) {
         const uint32_t ch0 = tid * CPT + rr * JPR, v = ch0 / CPR;
-        const bool have = int(v) < nv && pr[v];
-        Tab T;  // absent rows: any table times zero
-        load_tab(t.mtab, mul_index(E[v]), T);
+        const bool have = rhave[rr];
+        const Tab &T = RT[rr];
 #pragma unroll
         for (int j = 0; j < JPR; ++j) {
           const uint32_t c16 = ch0 % CPR + j;
@@ -299,20 +324,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
     exchange<LB, LA>(s, my, lane);
     fpassg<0, 4, L>(s, tabs, lbA());
 #pragma unroll
-    for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(s.l[r]), "+v"(s.h[r]));  // finished here, not sunk past the fill
-
-    // ---- output tables E[y], y < k, into the regions
-    __syncthreads();  // every wave is done with its region
-    uint32_t ftid = tid;
-    asm volatile("" : "+v"(ftid));  // table loads not hoisted into the transform
-#pragma unroll
-    for (int it = 0; it < 5; ++it) {  // k * 5 <= 2560 16-B chunks
-      const uint32_t i = ftid + it * THREADS;
-      if (i < uint32_t(k) * 5)
-        *reinterpret_cast<uint4 *>(regions + OutTabs::addr(i / 5, i % 5)) =
-            reinterpret_cast<const uint4 *>(t.mtab + mul_index(E[i / 5]))[i % 5];
-    }
-    __syncthreads();
+    for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(s.l[r]), "+v"(s.h[r]));  // finished here, not sunk into the output
 
     // ---- output (decode_main:185-188, reconstructSub:138-149): layout A,
     // lane -> codeword gi, y = y0 .. y0 + 15
@@ -333,7 +345,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
           const uint32_t y = y0 + r;
           const bool have = int(y) < nv && pr[y];
           Tab T;
-          OutTabs::load(regions, y, T);
+          OutTabs::load(outtabs, y, T);
           uint32_t ml = 0, mh = 0;
           mul_acc(s.l[r], s.h[r], T, ml, mh);
           uint32_t a = 0, c = 0;
@@ -393,7 +405,7 @@ hipError_t launch_l(const CodeParams &p, const DevTables &t, const uint8_t *d_sh
 }  // namespace
 
 bool decgen_applicable(const CodeParams &p) {
-  return p.n >= 64 && p.n <= 1024 && p.k >= 16 && p.k <= 512 && p.k % 16 == 0 && p.k < p.n;
+  return p.n >= 64 && p.n <= 1024 && p.k >= 16 && p.k <= 128 && p.k < p.n;
 }
 
 hipError_t launch_reconstruct_gen(const CodeParams &p, const DevTables &t,

@@ -60,7 +60,7 @@ hipError_t launch_encode_k1024(const CodeParams &p, const DevTables &t, const ui
                                size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                                size_t sstride, void *scratch, hipStream_t s);
 
-// register-blocked encode for k = 32 / 64 / 128, n <= 1024 (enc_gen.hip)
+// register-blocked encode for k = 16 .. 512, n <= 4096 (enc_gen.hip)
 bool encgen_applicable(const CodeParams &p);
 hipError_t launch_encode_gen(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                              size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,

@@ -1,5 +1,5 @@
-// enc_gen.hip — register-blocked encode for k = 2^M, M = 5..9 (k = 32 .. 512)
-// and n <= 4096: n_validators ~96..3069 outside the k = 256 / n = 1024 and
+// enc_gen.hip — register-blocked encode for k = 2^M, M = 4..9 (k = 16 .. 512)
+// and n <= 4096: n_validators 46..3069 outside the k = 256 / n = 1024 and
 // k = 1024 / n = 4096 kernels; this includes today's Polkadot validator counts
 // (k = 128, n = 1024 for 512..765 validators) and n = 2048 / 4096 with k = 256 / 512.
 //
@@ -237,10 +237,13 @@ __global__ void __launch_bounds__(THREADS)
     }
     const uint32_t lbA = tlin((16 * lane) & (Gm::K - 1));
     ipassg<0, (M < 4 ? M : 4), M>(s, tabs, lbA);
-    exchange<LA, LB>(s, my, lane);
-    if constexpr (M <= 8) {
+    if constexpr (M == 4) {
+      // k = 16: the whole IFFT is pass A; coefficients stay in layout A
+    } else if constexpr (M <= 8) {
+      exchange<LA, LB>(s, my, lane);
       ipassg<4, M - 4, M>(s, tabs, 0);
     } else {
+      exchange<LA, LB>(s, my, lane);
       ipassg<4, 4, M>(s, tabs, lbB(lane));
       exchange<LB, LC>(s, my, lane);
       ipassC9(s, tabs, 0);
@@ -257,14 +260,16 @@ __global__ void __launch_bounds__(THREADS)
 #pragma unroll
       for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(s.l[r]), "+v"(s.h[r]));
       const uint32_t lo = tlin(uint32_t(sh) & 1023u);  // tables at offset sh (disjoint bits)
-      if constexpr (M <= 8) {
+      if constexpr (M == 4) {
+      } else if constexpr (M <= 8) {
         fpassg<4, M - 4, M>(s, tabs, lo);
+        exchange<LB, LA>(s, my, lane);
       } else {
         fpassC9(s, tabs, lo);
         exchange<LC, LB>(s, my, lane);
         fpassg<4, 4, M>(s, tabs, lbB(lane) ^ lo);
+        exchange<LB, LA>(s, my, lane);
       }
-      exchange<LB, LA>(s, my, lane);
       fpassg<0, (M < 4 ? M : 4), M>(s, tabs, tlin((16 * lane) & (Gm::K - 1)) ^ lo);
       lds_barrier();  // all waves done with their regions (exchange, previous stores)
       stage<M>(s, my, lane);
@@ -301,13 +306,14 @@ hipError_t launch_m(const CodeParams &p, const DevTables &t, const uint8_t *d_pa
 }  // namespace
 
 bool encgen_applicable(const CodeParams &p) {
-  return p.k >= 32 && p.k <= 512 && (p.k & (p.k - 1)) == 0 && p.n <= 4096 && p.n >= 2 * p.k;
+  return p.k >= 16 && p.k <= 512 && (p.k & (p.k - 1)) == 0 && p.n <= 4096 && p.n >= 2 * p.k;
 }
 
 hipError_t launch_encode_gen(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                              size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                              size_t sstride, hipStream_t s) {
   switch (p.k) {
+    case 16: return launch_m<4>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
     case 32: return launch_m<5>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
     case 64: return launch_m<6>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
     case 128: return launch_m<7>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);

@@ -227,3 +227,26 @@ def test_host_batch_roundtrip(oracle, nv, plen, batch, chunk):
     for b in range(batch):
         assert out[b][:plen].tobytes() == pay[b].tobytes(), b
         assert not out[b][plen:].any()
+
+
+@pytest.mark.parametrize("nv", [600, 1024, 2500, 4096])
+def test_encode_shard_base_8_aligned(oracle, nv):
+    """Fast encodes with an 8-B (not 16-B) aligned shard base: 8-B stores."""
+    import torch
+    n, k, _ = E.code_params(nv)
+    plen, batch = 70001, 2
+    sl = E.shard_len(nv, plen)
+    ss = (sl + 15) // 16 * 16
+    ps = (plen + 15) // 16 * 16  # 16-B payload pitch: the fast kernels apply
+    pay = np.zeros((batch, ps), dtype=np.uint8)
+    for b in range(batch):
+        pay[b, :plen] = synth.payload(50 + b, plen)
+    d_pay = torch.from_numpy(pay).cuda()
+    raw = torch.zeros(batch * nv * ss + 8, dtype=torch.uint8, device="cuda")
+    d_sh = raw[8:]  # base 8 bytes past a 256-B aligned allocation
+    assert d_sh.data_ptr() % 16 == 8
+    E.encode_batch(nv, d_pay, plen, ps, batch, d_sh, ss)
+    torch.cuda.synchronize()
+    sh = d_sh.cpu().numpy().reshape(batch, nv, ss)[:, :, :sl]
+    for b in range(batch):
+        assert b"".join(oracle.encode(nv, pay[b, :plen].tobytes())) == sh[b].tobytes(), b
