@@ -23,7 +23,8 @@ except Exception:  # pragma: no cover
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "liberasure_coding_crust.so")
+# ECC_AMD_LIB: an alternative build of the same library (A/B kernel experiments)
+LIB_PATH = os.environ.get("ECC_AMD_LIB") or os.path.join(HERE, "lib", "liberasure_coding_crust.so")
 HEADERS = [os.path.join(os.path.dirname(HERE), "include", "erasure_coding", h)
            for h in ("erasure_coding.h", "ec_amd.h")]
 
