@@ -268,7 +268,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         } else {
 #pragma unroll
           for (int q = 0; q < 16; ++q) w[q] = 0;
-          #pragma unroll
+#pragma unroll
           for (int e = 0; e < 64; ++e)  // constant trip count: w stays in registers
             if (uint64_t(e) < avail) w[e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
         }

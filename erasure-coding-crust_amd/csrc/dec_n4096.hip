@@ -58,6 +58,45 @@ __device__ __forceinline__ uint32_t from_upper(uint32_t x, int b) {
   return r[1];
 }
 
+// multiplier logs (65535 = multiply by zero) of the linearised cross-quarter part
+struct Lin {
+  uint32_t p[4], k[4];
+};
+
+// Fold IFFT stages 10 (skews 1023 / 3071) and 11 (2047), the quarter bits of
+// the formal derivative and FFT stages 11 / 10 (a-side only) into
+// y = D(sum p_q u_q) + sum k_q u_q, by pushing u_q = 1 through them with the
+// reference's butterflies (additive_fft.hpp:99-141; skews[] == 0xFFFF: no
+// multiply).  Derivative quarter terms (poly_encoder.hpp:195-215):
+// c'0 = Dc0 + c1 + c2, c'1 = Dc1 + c3, c'2 = Dc2 + c3, c'3 = Dc3.
+Lin n4096_lin(int nq) {
+  const Field &f = field();
+  const auto mul = [&](uint16_t x, uint16_t c) -> uint16_t { return c == 0xFFFF ? 0 : f.mul(x, c); };
+  const uint16_t sa = f.skews[1023], sb = f.skews[3071], sc = f.skews[2047];
+  Lin lin{};
+  for (int q = 0; q < 4; ++q) {
+    uint16_t u[4] = {0, 0, 0, 0}, P = 0, Q = 0;
+    if (q < nq) u[q] = f.exp[0];  // the multiplicative identity
+    if (nq == 4) {
+      const uint16_t u1 = u[1] ^ u[0], u0 = u[0] ^ mul(u1, sa);
+      const uint16_t u3 = u[3] ^ u[2], u2 = u[2] ^ mul(u3, sb);
+      const uint16_t c2 = u2 ^ u0, c0 = u0 ^ mul(c2, sc);
+      const uint16_t c3 = u3 ^ u1, c1 = u1 ^ mul(c3, sc);
+      // y = c'0 + sc c'2 + sa (c'1 + sc c'3) = D(c0 + sa c1 + sc c2 + sa sc c3) + c1 + c2 + (sa + sc) c3
+      P = c0 ^ mul(c1, sa) ^ mul(c2, sc) ^ mul(mul(c3, sc), sa);
+      Q = c1 ^ c2 ^ mul(c3, sc) ^ mul(c3, sa);
+    } else {
+      const uint16_t c1 = u[1] ^ u[0], c0 = u[0] ^ mul(c1, sa);
+      // y = c'0 + sa c'1 = D(c0 + sa c1) + c1
+      P = c0 ^ mul(c1, sa);
+      Q = c1;
+    }
+    lin.p[q] = P ? f.log[P] : 65535u;
+    lin.k[q] = Q ? f.log[Q] : 65535u;
+  }
+  return lin;
+}
+
 }  // namespace
 
 // NQ = n / 1024 quarters (2 or 4); K = k (256, 512 or 1024)
@@ -70,7 +109,7 @@ reconstruct_n4096(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
     uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t K, uint32_t batch,
-    DevTables t) {
+    DevTables t, Lin lin) {
   constexpr int N = 1024 * NQ;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
@@ -91,23 +130,26 @@ reconstruct_n4096(
     const uint8_t *pr = present + b * N;
     const uint16_t *E = elog + b * N;
     uint8_t *O = out + b * ostride;
-    S16 Q[NQ];
+    S16 P, Qa;  // the two accumulators of the linearised cross-quarter stages
 
-    // ---- IFFT quarters 3, 2, 1, 0 (quarter 0's tables stay for the FFT); a
-    // lambda called per quarter so every Q[] index is a constant (a loop the
-    // unroller declines would leave Q in scratch memory)
-    const auto quarter = [&](S16 &Qq, const int q) __attribute__((always_inline)) {
+    // ---- IFFT quarters 3, 2, 1, 0 (quarter 0's tables stay for the FFT), each
+    // folded into P and Qa as soon as it is transformed
+    const auto quarter = [&](const int q) __attribute__((always_inline)) {
+      S16 Qq;
       __builtin_amdgcn_sched_barrier(0);
       lds_barrier();  // every wave is done with the tables and its region
+      uint32_t tq = tid;
+      asm volatile("" : "+v"(tq));  // this quarter's addresses and loads are not hoisted above here
+      const uint32_t lq = tq & 63;
       // the quarter's tables (skews 1024q + i) by LDS-DMA, in the background
       // of the row gather; retired before the barrier below
-      Tabs::dma_image<THREADS>(tabs, t.timg + q * kTabImageBytes, tid);
+      Tabs::dma_image<THREADS>(tabs, t.timg + q * kTabImageBytes, tq);
       __builtin_amdgcn_sched_barrier(0);
       // gather + scale the quarter's present rows (decode_main:174-177) into
       // the 8 groups' regions: thread -> rows 1024q + tid, + 512
 #pragma unroll
       for (int half = 0; half < 1024 / THREADS; ++half) {
-        const uint32_t vl = tid + half * THREADS, v = 1024 * q + vl;
+        const uint32_t vl = tq + half * THREADS, v = 1024 * q + vl;
         uint32_t l[8], h[8];
 #pragma unroll
         for (int g = 0; g < 8; ++g) l[g] = h[g] = 0;
@@ -125,11 +167,7 @@ reconstruct_n4096(
               w[4 * j + 3] = d.w;
             }
           } else {
-#pragma unroll
-            for (int j = 0; j < 16; ++j) w[j] = 0;
-            #pragma unroll
-            for (int e = 0; e < 64; ++e)  // constant trip count: w stays in registers
-              if (uint64_t(e) < avail) w[e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
+            load_row_tail64(row, avail, w);
           }
           Tab T;
           load_tab(t.mtab, mul_index(E[v]), T);
@@ -149,95 +187,72 @@ reconstruct_n4096(
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(posA(lane, r)));
+        const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(posA(lq, r)));
         Qq.l[r] = x.x;
         Qq.h[r] = x.y;
       }
-      ifft1024(Qq, tabs, my, lane);  // -> layout C
+      ifft1024(Qq, tabs, my, lq);  // -> layout C
+      __builtin_amdgcn_sched_barrier(0);
+      Tab TP, TK;
+      uint32_t ip = lin.p[q], ik = lin.k[q];
+      asm volatile("" : "+s"(ip), "+s"(ik));  // loaded here, not hoisted (and kept live) from the top
+      load_tab(t.mtab, ip, TP);
+      load_tab(t.mtab, ik, TK);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (q == NQ - 1) P.l[r] = P.h[r] = Qa.l[r] = Qa.h[r] = 0;
+        mul_acc(Qq.l[r], Qq.h[r], TP, P.l[r], P.h[r]);
+        mul_acc(Qq.l[r], Qq.h[r], TK, Qa.l[r], Qa.h[r]);  // shares the selectors of the line above
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r)  // accumulated here, not sunk into the next quarter's gather
+        asm volatile("" : "+v"(P.l[r]), "+v"(P.h[r]), "+v"(Qa.l[r]), "+v"(Qa.h[r]));
       __builtin_amdgcn_sched_barrier(0);
     };
     if constexpr (NQ == 4) {
-      quarter(Q[NQ - 1], 3);
-      quarter(Q[NQ - 2], 2);
+      quarter(3);
+      quarter(2);
     }
-    quarter(Q[1], 1);
-    quarter(Q[0], 0);
+    quarter(1);
+    quarter(0);
 
-    // ---- IFFT stages 10 (skews 1023 / 3071) and 11 (skew 2047) across quarters
-    Tab T10a, T10b, T11;
-    load_tab(t.mtab, t.skews[1023], T10a);
+    // ---- cross-quarter IFFT stages (10, 11), the quarter bits of the formal
+    // derivative and FFT stages 11 / 10 on the side that reaches y < 1024 are
+    // all GF-linear with constant multipliers, so the FFT_1024 input is
+    //   y = D(P) + Qa,  P = sum_q p_q u_q,  Qa = sum_q k_q u_q
+    // (u_q = IFFT_1024 of quarter q, D = the within-quarter derivative, p_q /
+    // k_q folded on the host from skews 1023 / 2047 / 3071: n4096_lin()).
+    // D in closed form (poly_encoder.hpp:195-215) over bits 0..9, in place:
+    // lane = p0..p5, r = (p8, p9, p6, p7).
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      Q[1].l[r] ^= Q[0].l[r];
-      Q[1].h[r] ^= Q[0].h[r];
-      mul_acc(Q[1].l[r], Q[1].h[r], T10a, Q[0].l[r], Q[0].h[r]);
-    }
-    if constexpr (NQ == 4) {
-      load_tab(t.mtab, t.skews[3071], T10b);
-      load_tab(t.mtab, t.skews[2047], T11);
+      uint32_t al = 0, ah = 0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        Q[NQ - 1].l[r] ^= Q[NQ - 2].l[r];
-        Q[NQ - 1].h[r] ^= Q[NQ - 2].h[r];
-        mul_acc(Q[NQ - 1].l[r], Q[NQ - 1].h[r], T10b, Q[NQ - 2].l[r], Q[NQ - 2].h[r]);
+      for (int lb = 0; lb < 6; ++lb) {
+        const uint32_t m = ((lane >> lb) & 1) ? 0u : 0xffffffffu;
+        al ^= from_upper(P.l[r], lb) & m;
+        ah ^= from_upper(P.h[r], lb) & m;
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          Q[q + NQ - 2].l[r] ^= Q[q].l[r];
-          Q[q + NQ - 2].h[r] ^= Q[q].h[r];
-          mul_acc(Q[q + NQ - 2].l[r], Q[q + NQ - 2].h[r], T11, Q[q].l[r], Q[q].h[r]);
+      for (int rb = 0; rb < 4; ++rb)
+        if (!(r & (1 << rb))) {
+          al ^= P.l[r | (1 << rb)];
+          ah ^= P.h[r | (1 << rb)];
         }
-      }
+      P.l[r] ^= al;
+      P.h[r] ^= ah;
+    }
+    S16 Y;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      Y.l[r] = P.l[r] ^ Qa.l[r];
+      Y.h[r] = P.h[r] ^ Qa.h[r];
     }
 
-    // ---- formal derivative, closed form, in place in increasing (q, r) order:
-    // register partners (q, r | 2^rb) and quarter partners (q | 2^qb, r) are
-    // still original when (q, r) is processed; lane partners read the other
-    // lanes' original (q, r).  Bits: lane = p0..p5, r = (p8, p9, p6, p7), q = (p10, p11).
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        uint32_t al = 0, ah = 0;
-#pragma unroll
-        for (int lb = 0; lb < 6; ++lb) {
-          const uint32_t m = ((lane >> lb) & 1) ? 0u : 0xffffffffu;
-          al ^= from_upper(Q[q].l[r], lb) & m;
-          ah ^= from_upper(Q[q].h[r], lb) & m;
-        }
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-          if (!(r & (1 << rb))) {
-            al ^= Q[q].l[r | (1 << rb)];
-            ah ^= Q[q].h[r | (1 << rb)];
-          }
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-          if ((1 << qb) < NQ && !(q & (1 << qb))) {
-            al ^= Q[q | (1 << qb)].l[r];
-            ah ^= Q[q | (1 << qb)].h[r];
-          }
-        Q[q].l[r] ^= al;
-        Q[q].h[r] ^= ah;
-      }
-    }
-
-    // ---- FFT stage 11 (keep v < 2048) and stage 10 (keep v < 1024): a ^= b * s
-    if constexpr (NQ == 4) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        mul_acc(Q[NQ - 2].l[r], Q[NQ - 2].h[r], T11, Q[0].l[r], Q[0].h[r]);
-        mul_acc(Q[NQ - 1].l[r], Q[NQ - 1].h[r], T11, Q[1].l[r], Q[1].h[r]);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) mul_acc(Q[1].l[r], Q[1].h[r], T10a, Q[0].l[r], Q[0].h[r]);
     // ---- FFT_1024, index 0, on quarter 0 (tables of quarter 0 still resident)
-    fft1024(Q[0], tabs, my, lane);  // -> layout A: y = 16 lane + r
+    fft1024(Y, tabs, my, lane);  // -> layout A: y = 16 lane + r
 #pragma unroll
-    for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(Q[0].l[r]), "+v"(Q[0].h[r]));  // not sunk past the table gather
+    for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(Y.l[r]), "+v"(Y.h[r]));  // not sunk past the table gather
 
     // ---- output (decode_main:185-188, reconstructSub:138-149): erased y < k
     // scaled by E[y] (tables now in LDS), present y copied from the shard
@@ -269,7 +284,7 @@ reconstruct_n4096(
         } else {
           Tab T;
           Tabs::load(tabs, y, T);
-          mul_acc(Q[0].l[r], Q[0].h[r], T, ol[r], oh[r]);
+          mul_acc(Y.l[r], Y.h[r], T, ol[r], oh[r]);
         }
       }
       // column c: y = 16 lane .. 16 lane + 15 -> 32 contiguous bytes (BE symbols)
@@ -313,14 +328,15 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
   }
   const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
+  static const Lin lin4 = n4096_lin(4), lin2 = n4096_lin(2);
   if (p.n == 4096)
     hipLaunchKernelGGL(reconstruct_n4096<4>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
                        uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out,
-                       uint64_t(ostride), int(p.nv), uint32_t(p.k), uint32_t(batch), t);
+                       uint64_t(ostride), int(p.nv), uint32_t(p.k), uint32_t(batch), t, lin4);
   else
     hipLaunchKernelGGL(reconstruct_n4096<2>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
                        uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out,
-                       uint64_t(ostride), int(p.nv), uint32_t(p.k), uint32_t(batch), t);
+                       uint64_t(ostride), int(p.nv), uint32_t(p.k), uint32_t(batch), t, lin2);
   return hipGetLastError();
 }
 

@@ -33,6 +33,22 @@ __device__ __forceinline__ uint32_t vperm(uint32_t hi, uint32_t lo, uint32_t sel
 // whose fence drains vmcnt and would serialize the HBM write stream with the
 // next tile's compute.  The asm "memory" clobbers stop compiler reordering of
 // LDS accesses across the barrier.
+// bytes [0, avail) (avail < 64) of a 4-B aligned row slice into w[16], zero
+// beyond: dword loads for whole dwords, bytes for the last partial one (nothing
+// past the row's end is read).  Constant indices only, so w stays in registers
+// and at most 16 loads are in flight.
+__device__ __forceinline__ void load_row_tail64(const uint8_t *row, uint64_t avail, uint32_t (&w)[16]) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    w[j] = 0;
+    if (uint64_t(4 * j + 4) <= avail) {
+      w[j] = reinterpret_cast<const uint32_t *>(row)[j];
+    } else if (uint64_t(4 * j) < avail) {
+      for (uint32_t e = 0; 4 * j + e < avail; ++e) w[j] |= uint32_t(row[4 * j + e]) << (8 * e);
+    }
+  }
+}
+
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
