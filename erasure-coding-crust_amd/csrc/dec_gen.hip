@@ -175,7 +175,115 @@ __device__ __forceinline__ void derivative(S16 &s, uint32_t lane) {
   }
 }
 
-template <int L>
+
+// ---- FFT_n restricted to the outputs y < k = 2^KB (afft, additive_fft.hpp:121-141),
+// from the layout the derivative ran in (X = C for n >= 512, B below):
+//  * register-held stages t >= KB keep only the side that reaches y < k
+//    (a ^= b * s); registers with such a bit set are dead afterwards;
+//  * register-held stages below KB are full butterflies on the live registers;
+//  * the lane-held stages (p5..p0 in C, p3..p0 in B) run in registers after
+//    swapping each lane bit with register bit SB (the one of p6 / p4, whose
+//    stage is done) by DPP / v_permlane*_swap: no LDS exchange.
+// Afterwards: SB = p0, lane bits 0.. = p1.., the other register bits unchanged.
+template <Layout X>
+__host__ __device__ constexpr int rbit_of(int p) {
+  return reg_pbit<X>(0) == p ? 0 : reg_pbit<X>(1) == p ? 1 : reg_pbit<X>(2) == p ? 2
+                                 : reg_pbit<X>(3) == p ? 3 : -1;
+}
+// register r is still needed after the a-only stages above t (t = KB - 1: all)
+template <Layout X, int L, int KB>
+__host__ __device__ constexpr bool live_above(int r, int t) {
+  for (int p = (t + 1 > KB ? t + 1 : KB); p < L; ++p) {
+    const int b = rbit_of<X>(p);
+    if (b >= 0 && ((r >> b) & 1)) return false;
+  }
+  return true;
+}
+// local position bits held in register r (register bit skip excluded)
+template <Layout X, int L>
+__host__ __device__ constexpr uint32_t reg_pos(int r, int skip) {
+  uint32_t v = 0;
+  for (int b = 0; b < 4; ++b)
+    if (b != skip && ((r >> b) & 1) && reg_pbit<X>(b) < L) v |= 1u << reg_pbit<X>(b);
+  return v;
+}
+template <Layout X>
+__host__ __device__ constexpr int swap_rbit() { return X == LC ? 2 : 0; }  // p6 / p4
+template <Layout X>
+__host__ __device__ constexpr int lane_stages() { return X == LC ? 6 : 4; }  // p0..p5 / p0..p3
+
+// swap register bit (x: bit 0, y: bit 1) with lane bit b; hi = this lane's bit b
+__device__ __forceinline__ void swap_bit(uint32_t &x, uint32_t &y, int b, bool hi) {
+  if (b == 4) {
+    auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+    return;
+  }
+  if (b == 5) {
+    auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+    return;
+  }
+  const uint32_t send = hi ? x : y;  // lane bit 1 sends x, lane bit 0 sends y
+  uint32_t recv;
+  switch (b) {
+    case 0: recv = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0xB1, 0xf, 0xf, true)); break;  // quad [1,0,3,2]
+    case 1: recv = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x4E, 0xf, 0xf, true)); break;  // quad [2,3,0,1]
+    case 2: {
+      const uint32_t up = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x104, 0xf, 0xf, true));
+      const uint32_t dn = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x114, 0xf, 0xf, true));
+      recv = hi ? dn : up;
+      break;
+    }
+    default: recv = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x128, 0xf, 0xf, true)); break;  // row_ror:8
+  }
+  if (hi) x = recv;
+  else y = recv;
+}
+
+template <Layout X, int L, int KB>
+__device__ __forceinline__ void fft_restricted(S16 &s, const uint8_t *tabs, uint32_t lane) {
+  constexpr int F = X == LC ? 6 : 4;  // lowest register-held position bit
+  constexpr int SB = swap_rbit<X>(), NL = lane_stages<X>();
+  // register-held stages L-1 .. F (tables: wave-uniform, from the register bits above t)
+#pragma unroll
+  for (int t = L - 1; t >= F; --t) {
+    const int b = rbit_of<X>(t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (((r >> b) & 1) || !live_above<X, L, KB>(r, t)) continue;
+      Tab T;
+      tab_at(tabs, tlin(skew_idx(reg_pos<X, L>(r, -1), t)), T);
+      if (t >= KB) mul_acc(s.l[r | (1 << b)], s.h[r | (1 << b)], T, s.l[r], s.h[r]);  // a-side only
+      else fb(s, r, r | (1 << b), T);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // lane-held stages NL-1 .. 0: swap lane bit u into register bit SB, butterfly
+#pragma unroll
+  for (int u = NL - 1; u >= 0; --u) {
+    uint32_t l = lane;
+    asm volatile("" : "+v"(l));
+    const bool hi = (l >> u) & 1;
+    // bits above u now: p(u+1)..p(NL) in lane bits u..NL-1, the rest in registers
+    const uint32_t lane_hi = ((l & ((1u << NL) - 1)) >> u) << (u + 1);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (((r >> SB) & 1) || !live_above<X, L, KB>(r & ~(1 << SB), KB - 1)) continue;
+      const int r1 = r | (1 << SB);
+      swap_bit(s.l[r], s.l[r1], u, hi);
+      swap_bit(s.h[r], s.h[r1], u, hi);
+      Tab T;
+      tab_at(tabs, tlin(skew_idx((lane_hi | reg_pos<X, L>(r, SB)) & ((1u << L) - 1), u)), T);
+      fb(s, r, r1, T);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int L, int KB>
 __global__ void __launch_bounds__(THREADS) reconstruct_gen(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
@@ -305,8 +413,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
       __builtin_amdgcn_sched_barrier(0);
       derivative<LB, L>(s, lane);
       __builtin_amdgcn_sched_barrier(0);
-      fpassg<4, L - 4, L>(s, tabs, lbB());
-      __builtin_amdgcn_sched_barrier(0);
+      fft_restricted<LB, L, KB>(s, tabs, lane);
     } else {
       ipassg<4, 4, L>(s, tabs, lbB());
       __builtin_amdgcn_sched_barrier(0);
@@ -315,39 +422,42 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
       __builtin_amdgcn_sched_barrier(0);
       derivative<LC, L>(s, lane);
       __builtin_amdgcn_sched_barrier(0);
-      fpassCg<L>(s, tabs);
-      __builtin_amdgcn_sched_barrier(0);
-      exchange<LC, LB>(s, my, lane);
-      fpassg<4, 4, L>(s, tabs, lbB());
-      __builtin_amdgcn_sched_barrier(0);
+      fft_restricted<LC, L, KB>(s, tabs, lane);
     }
-    exchange<LB, LA>(s, my, lane);
-    fpassg<0, 4, L>(s, tabs, lbA());
 #pragma unroll
     for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(s.l[r]), "+v"(s.h[r]));  // finished here, not sunk into the output
 
-    // ---- output (decode_main:185-188, reconstructSub:138-149): layout A,
-    // lane -> codeword gi, y = y0 .. y0 + 15
+    // ---- output (decode_main:185-188, reconstructSub:138-149): every live
+    // register pair (r: p0 = 0, r | SB: p0 = 1) holds y0, y0 + 1 of one codeword
+    // (position = p0 | lane bits 0.. -> p1.. | other register bits | in layout B
+    // lane bits 4, 5 -> p8, p9); 4 bytes per column
+    {
+      constexpr Layout X = L <= 8 ? LB : LC;
+      constexpr int SB = swap_rbit<X>(), NL = lane_stages<X>();
+      uint32_t olane = lane;
+      asm volatile("" : "+v"(olane));  // output addresses / shard re-reads not hoisted over the transform
 #pragma unroll
-    for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(s.l[r]), "+v"(s.h[r]));  // mul_acc selects stay here
-    uint32_t olane = lane;
-    asm volatile("" : "+v"(olane));  // output addresses / shard re-reads not hoisted over the transform
-    const uint32_t gi = (16 * olane) >> L, y0 = (16 * olane) & NM;
-    if (y0 < uint32_t(k)) {
-      const uint64_t cbase = col0 + 4 * (uint64_t(wave) * INST + gi);
-      const bool full = cbase + 4 <= ncols;  // else the tile's last, partial group
+      for (int r = 0; r < 16; ++r) {
+        if (((r >> SB) & 1) || !live_above<X, L, KB>(r & ~(1 << SB), KB - 1)) continue;
+        uint32_t pos = ((olane & ((1u << NL) - 1)) << 1);
 #pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {  // 4 registers = 4 consecutive y at a time
-        uint32_t ol[4], oh[4];
+        for (int bb = 0; bb < 4; ++bb)
+          if (bb != SB && ((r >> bb) & 1)) pos |= 1u << reg_pbit<X>(bb);
+        if constexpr (X == LB) pos |= ((olane >> 4) & 3) << 8;
+        const uint32_t gi = pos >> L, y0 = pos & NM;
+        if (y0 >= uint32_t(k)) continue;
+        const uint64_t cbase = col0 + 4 * (uint64_t(wave) * INST + gi);
+        const bool full = cbase + 4 <= ncols;  // else the tile's last, partial group
+        uint32_t ol[2], oh[2];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = 4 * q4 + q;
-          const uint32_t y = y0 + r;
+        for (int q = 0; q < 2; ++q) {
+          const int rq = q ? (r | (1 << SB)) : r;
+          const uint32_t y = y0 + q;
           const bool have = int(y) < nv && pr[y];
           Tab T;
           OutTabs::load(outtabs, y, T);
           uint32_t ml = 0, mh = 0;
-          mul_acc(s.l[r], s.h[r], T, ml, mh);
+          mul_acc(s.l[rq], s.h[rq], T, ml, mh);
           uint32_t a = 0, c = 0;
           const uint8_t *row = SH + uint64_t(have ? y : 0u) * sstride + 2 * cbase;
           if (full) {
@@ -364,14 +474,12 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
           ol[q] = have ? vperm(c, a, 0x07050301u) : ml;
         }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {  // column c: 4 consecutive y -> 8 bytes BE
+        for (int c = 0; c < 4; ++c) {  // column c: y0, y0 + 1 -> 4 bytes BE
           const uint64_t col = cbase + c;
           if (col >= ncols) break;
-          const uint32_t w0 = vperm(ol[0], oh[0], 0x0c0c0400u + 0x0101u * c) |
-                              (vperm(ol[1], oh[1], 0x0c0c0400u + 0x0101u * c) << 16);
-          const uint32_t w1 = vperm(ol[2], oh[2], 0x0c0c0400u + 0x0101u * c) |
-                              (vperm(ol[3], oh[3], 0x0c0c0400u + 0x0101u * c) << 16);
-          *reinterpret_cast<uint2 *>(O + (col * uint64_t(k) + y0 + 4 * q4) * 2) = make_uint2(w0, w1);
+          *reinterpret_cast<uint32_t *>(O + (col * uint64_t(k) + y0) * 2) =
+              vperm(ol[0], oh[0], 0x0c0c0400u + 0x0101u * c) |
+              (vperm(ol[1], oh[1], 0x0c0c0400u + 0x0101u * c) << 16);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -379,7 +487,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
   }
 }
 
-template <int L>
+template <int L, int KB>
 hipError_t launch_l(const CodeParams &p, const DevTables &t, const uint8_t *d_shards, size_t slen,
                     size_t sstride, const uint8_t *d_present, const uint16_t *d_err_log,
                     size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
@@ -389,14 +497,14 @@ hipError_t launch_l(const CodeParams &p, const DevTables &t, const uint8_t *d_sh
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&reconstruct_gen<L>),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&reconstruct_gen<L, KB>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return e;
   }
   constexpr int TC = WAVES * 4 * (1024 >> L);
   const size_t tiles = (slen / 2 + TC - 1) / TC * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
-  hipLaunchKernelGGL(reconstruct_gen<L>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
+  hipLaunchKernelGGL((reconstruct_gen<L, KB>), dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
                      uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out,
                      uint64_t(ostride), int(p.nv), int(p.k), uint32_t(batch), t);
   return hipGetLastError();
@@ -404,21 +512,31 @@ hipError_t launch_l(const CodeParams &p, const DevTables &t, const uint8_t *d_sh
 
 }  // namespace
 
-bool decgen_applicable(const CodeParams &p) {
-  return p.n >= 64 && p.n <= 1024 && p.k >= 16 && p.k <= 128 && p.k < p.n;
+bool decgen_applicable(const CodeParams &p) {  // the (n, k) instantiated below
+  return (p.n == 64 && p.k == 16) || (p.n == 128 && (p.k == 16 || p.k == 32)) ||
+         (p.n == 256 && (p.k == 32 || p.k == 64)) || (p.n == 512 && (p.k == 64 || p.k == 128)) ||
+         (p.n == 1024 && p.k == 128);
 }
 
 hipError_t launch_reconstruct_gen(const CodeParams &p, const DevTables &t,
                                   const uint8_t *d_shards, size_t slen, size_t sstride,
                                   const uint8_t *d_present, const uint16_t *d_err_log,
                                   size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
-  switch (p.n) {
-    case 64: return launch_l<6>(p, t, d_shards, slen, sstride, d_present, d_err_log, batch, d_out, ostride, s);
-    case 128: return launch_l<7>(p, t, d_shards, slen, sstride, d_present, d_err_log, batch, d_out, ostride, s);
-    case 256: return launch_l<8>(p, t, d_shards, slen, sstride, d_present, d_err_log, batch, d_out, ostride, s);
-    case 512: return launch_l<9>(p, t, d_shards, slen, sstride, d_present, d_err_log, batch, d_out, ostride, s);
-    default: return launch_l<10>(p, t, d_shards, slen, sstride, d_present, d_err_log, batch, d_out, ostride, s);
-  }
+#define ECAMD_DG(Lv, KBv)                                                                   \
+  if (p.n == (1u << Lv) && p.k == (1u << KBv))                                             \
+    return launch_l<Lv, KBv>(p, t, d_shards, slen, sstride, d_present, d_err_log, batch, d_out, \
+                             ostride, s);
+  // every (n, k) of 46 <= n_validators <= 765 (decgen_applicable)
+  ECAMD_DG(6, 4)
+  ECAMD_DG(7, 4)
+  ECAMD_DG(7, 5)
+  ECAMD_DG(8, 5)
+  ECAMD_DG(8, 6)
+  ECAMD_DG(9, 6)
+  ECAMD_DG(9, 7)
+  ECAMD_DG(10, 7)
+#undef ECAMD_DG
+  return hipErrorInvalidValue;
 }
 
 }  // namespace ecamd
