@@ -8,14 +8,16 @@
 // FFT_4096 of which the k = 1024 outputs y < k are read.  Structure used:
 //  * IFFT_4096 stages 0..9 act inside each quarter q (positions 1024q ..
 //    1024q + 1023) with skew indices 1024q + (0..1022): four IFFT_1024 (tf1024.hpp)
-//    with per-quarter tables, then stages 10 and 11 across the quarters in
-//    registers (skews 1023 / 3071 and 2047);
-//  * the derivative in closed form c'[j] = c[j] ^ XOR_{b: j_b = 0} c[j | 2^b]
-//    (poly_encoder.hpp:195-215), in place over the 64 registers and the lane bits;
-//  * FFT stages 11 and 10 only on the side that reaches y < 1024, then one
-//    FFT_1024 (index 0) on quarter 0.
-// A wave owns one byte-planar group (4 columns) for the whole tile: 4 quarters
-// x 16 registers in layout C.  The workgroup (8 waves, 32 columns) shares one
+//    with per-quarter tables;
+//  * IFFT stages 10 / 11 across the quarters, the quarter bits of the formal
+//    derivative and FFT stages 11 / 10 on the side that reaches y < 1024 are
+//    folded into two accumulators (constants from the host, n4096_lin), each
+//    quarter added in as soon as it is transformed; the within-quarter
+//    derivative in closed form c'[j] = c[j] ^ XOR_{b < 10: j_b = 0} c[j | 2^b]
+//    (poly_encoder.hpp:195-215);
+//  * one FFT_1024 (index 0): whole for k = 1024, restricted to y < k otherwise.
+// A wave owns one byte-planar group (4 columns) for the whole tile, in layout
+// C.  The workgroup (8 waves, 32 columns) shares one
 // 80 KB multiply-table set in LDS, reloaded per quarter (3, 2, 1, then 0, which
 // stays for the FFT) and finally replaced by the output tables E[y], y < k.
 #include <hip/hip_runtime.h>
@@ -37,26 +39,6 @@ constexpr int LDS_BYTES = Tabs::kBytes + WAVES * REG_BYTES;
 static_assert(LDS_BYTES <= 160 * 1024 && Tabs::kBytes == kTabImageBytes, "LDS budget");
 
 __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ? 0u : c; }
-
-__device__ __forceinline__ uint32_t dpp_up(uint32_t x, int b) {  // value of lane + 2^b (b < 4)
-  switch (b) {
-    case 0: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x101, 0xf, 0xf, true));
-    case 1: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x102, 0xf, 0xf, true));
-    case 2: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x104, 0xf, 0xf, true));
-    default: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x108, 0xf, 0xf, true));
-  }
-}
-
-// value of lane (lane + 2^b) for lanes whose bit b is 0 (others: don't care)
-__device__ __forceinline__ uint32_t from_upper(uint32_t x, int b) {
-  if (b < 4) return dpp_up(x, b);
-  if (b == 4) {
-    auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-    return r[1];
-  }
-  auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-  return r[1];
-}
 
 // multiplier logs (65535 = multiply by zero) of the linearised cross-quarter part
 struct Lin {
@@ -99,8 +81,8 @@ Lin n4096_lin(int nq) {
 
 }  // namespace
 
-// NQ = n / 1024 quarters (2 or 4); K = k (256, 512 or 1024)
-template <int NQ>
+// NQ = n / 1024 quarters (2 or 4); K = k = 2^KB (256, 512 or 1024)
+template <int NQ, int KB>
 __global__ void __launch_bounds__(THREADS)
 #if DEC4_WAVES == 4
 __attribute__((amdgpu_waves_per_eu(1, 1)))
@@ -224,24 +206,7 @@ reconstruct_n4096(
     // k_q folded on the host from skews 1023 / 2047 / 3071: n4096_lin()).
     // D in closed form (poly_encoder.hpp:195-215) over bits 0..9, in place:
     // lane = p0..p5, r = (p8, p9, p6, p7).
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      uint32_t al = 0, ah = 0;
-#pragma unroll
-      for (int lb = 0; lb < 6; ++lb) {
-        const uint32_t m = ((lane >> lb) & 1) ? 0u : 0xffffffffu;
-        al ^= from_upper(P.l[r], lb) & m;
-        ah ^= from_upper(P.h[r], lb) & m;
-      }
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-        if (!(r & (1 << rb))) {
-          al ^= P.l[r | (1 << rb)];
-          ah ^= P.h[r | (1 << rb)];
-        }
-      P.l[r] ^= al;
-      P.h[r] ^= ah;
-    }
+    derivative<LC, 10>(P, lane);
     S16 Y;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -249,8 +214,11 @@ reconstruct_n4096(
       Y.h[r] = P.h[r] ^ Qa.h[r];
     }
 
-    // ---- FFT_1024, index 0, on quarter 0 (tables of quarter 0 still resident)
-    fft1024(Y, tabs, my, lane);  // -> layout A: y = 16 lane + r
+    // ---- FFT_1024, index 0 (quarter 0's tables still resident): whole for
+    // k = 1024 (-> layout A: y = 16 lane + r), else restricted to y < k
+    // (tf1024.hpp fft_restricted: live register pairs hold y0, y0 + 1)
+    if constexpr (KB == 10) fft1024(Y, tabs, my, lane);
+    else fft_restricted<LC, 10, KB>(Y, tabs, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(Y.l[r]), "+v"(Y.h[r]));  // not sunk past the table gather
 
@@ -260,7 +228,51 @@ reconstruct_n4096(
     Tabs::gather<THREADS>(tabs, t.mtab, [&](uint32_t y) { return mul_index(E[y]); }, tid);
     lds_barrier();
     const uint64_t cbase = col0 + 4 * wave;
-    if (16 * lane < K) {  // k < 1024: the other lanes' y are not read
+    if constexpr (KB < 10) {
+      constexpr int SB = swap_rbit<LC>();
+      uint32_t olane = lane;
+      asm volatile("" : "+v"(olane));
+      const bool full = cbase + 4 <= ncols;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (((r >> SB) & 1) || !live_above<LC, 10, KB>(r & ~(1 << SB), KB - 1)) continue;
+        const uint32_t y0 = (olane << 1) | reg_pos<LC, 10>(r, SB);
+        uint32_t ol[2], oh[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int rq = q ? (r | (1 << SB)) : r;
+          const uint32_t y = y0 + q;
+          const bool have = int(y) < nv && pr[y];
+          Tab T;
+          Tabs::load(tabs, y, T);
+          uint32_t ml = 0, mh = 0;
+          mul_acc(Y.l[rq], Y.h[rq], T, ml, mh);
+          uint32_t a = 0, c = 0;
+          const uint8_t *row = SH + uint64_t(have ? y : 0u) * sstride + 2 * cbase;
+          if (full) {
+            const uint2 d = *reinterpret_cast<const uint2 *>(row);
+            a = d.x;
+            c = d.y;
+          } else if (have && cbase < ncols) {
+            for (uint64_t e = 0; e < 2 * (ncols - cbase); ++e) {
+              if (e < 4) a |= uint32_t(row[e]) << (8 * e);
+              else c |= uint32_t(row[e]) << (8 * (e - 4));
+            }
+          }
+          oh[q] = have ? vperm(c, a, 0x06040200u) : mh;
+          ol[q] = have ? vperm(c, a, 0x07050301u) : ml;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {  // column c: y0, y0 + 1 -> 4 bytes BE
+          const uint64_t col = cbase + c;
+          if (col >= ncols) break;
+          *reinterpret_cast<uint32_t *>(O + (col * uint64_t(K) + y0) * 2) =
+              vperm(ol[0], oh[0], 0x0c0c0400u + 0x0101u * c) |
+              (vperm(ol[1], oh[1], 0x0c0c0400u + 0x0101u * c) << 16);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
       uint32_t ol[16], oh[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -305,8 +317,8 @@ reconstruct_n4096(
   }
 }
 
-bool n4096_applicable(const CodeParams &p) {
-  return (p.n == 4096 || p.n == 2048) && p.k >= 256 && p.k <= 1024;
+bool n4096_applicable(const CodeParams &p) {  // the (n, k) instantiated below
+  return (p.n == 4096 && (p.k == 1024 || p.k == 512)) || (p.n == 2048 && (p.k == 512 || p.k == 256));
 }
 
 hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
@@ -319,24 +331,31 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&reconstruct_n4096<4>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&reconstruct_n4096<2>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    if (e != hipSuccess) return e;
+    const void *fns[] = {reinterpret_cast<const void *>(&reconstruct_n4096<4, 10>),
+                         reinterpret_cast<const void *>(&reconstruct_n4096<4, 9>),
+                         reinterpret_cast<const void *>(&reconstruct_n4096<2, 9>),
+                         reinterpret_cast<const void *>(&reconstruct_n4096<2, 8>)};
+    for (const void *f : fns) {
+      const hipError_t e =
+          hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      if (e != hipSuccess) return e;
+    }
   }
   const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   static const Lin lin4 = n4096_lin(4), lin2 = n4096_lin(2);
-  if (p.n == 4096)
-    hipLaunchKernelGGL(reconstruct_n4096<4>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
-                       uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out,
-                       uint64_t(ostride), int(p.nv), uint32_t(p.k), uint32_t(batch), t, lin4);
-  else
-    hipLaunchKernelGGL(reconstruct_n4096<2>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
-                       uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out,
-                       uint64_t(ostride), int(p.nv), uint32_t(p.k), uint32_t(batch), t, lin2);
+#define ECAMD_D4(NQv, KBv)                                                                    \
+  if (p.n == 1024u * NQv && p.k == (1u << KBv))                                                  \
+    hipLaunchKernelGGL((reconstruct_n4096<NQv, KBv>), dim3(grid), dim3(THREADS), LDS_BYTES, s,   \
+                       d_shards, uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out, \
+                       uint64_t(ostride), int(p.nv), uint32_t(p.k), uint32_t(batch), t,         \
+                       NQv == 4 ? lin4 : lin2);
+  ECAMD_D4(4, 10)
+  else ECAMD_D4(4, 9)
+  else ECAMD_D4(2, 9)
+  else ECAMD_D4(2, 8)
+  else return hipErrorInvalidValue;
+#undef ECAMD_D4
   return hipGetLastError();
 }
 

@@ -192,6 +192,178 @@ __device__ __forceinline__ void fft1024(S16 &s, const uint8_t *tabs, uint8_t *my
   fpass4<0>(s, tabs, tlin(16 * lane));
 }
 
+// ---- cross-lane helpers, layout bit maps, closed-form derivative and the
+// restricted FFT (reconstruct_gen, reconstruct_n4096)
+__device__ __forceinline__ uint32_t dpp_up(uint32_t x, int b) {  // value of lane + 2^b (b < 4)
+  switch (b) {
+    case 0: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x101, 0xf, 0xf, true));
+    case 1: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x102, 0xf, 0xf, true));
+    case 2: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x104, 0xf, 0xf, true));
+    default: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x108, 0xf, 0xf, true));
+  }
+}
+
+// value of lane (lane + 2^b) for lanes whose bit b is 0 (others: don't care)
+__device__ __forceinline__ uint32_t from_upper(uint32_t x, int b) {
+  if (b < 4) return dpp_up(x, b);
+  if (b == 4) {
+    auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return r[1];
+  }
+  auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return r[1];
+}
+
+// position bit held by register bit t / lane bit u in each layout (tf1024.hpp)
+template <Layout X>
+__host__ __device__ constexpr int reg_pbit(int t) {
+  if constexpr (X == LA) return t;
+  else if constexpr (X == LB) return t + 4;
+  else return t == 0 ? 8 : t == 1 ? 9 : t == 2 ? 6 : 7;
+}
+template <Layout X>
+__host__ __device__ constexpr int lane_pbit(int u) {
+  if constexpr (X == LB) return u < 4 ? u : u + 4;
+  else if constexpr (X == LA) return u + 4;
+  else return u;
+}
+
+
+// formal derivative (poly_encoder.hpp:195-215), closed form, in layout X, in
+// place: registers in increasing order (register partners r | 2^t > r are
+// still original), lane partners read the other lanes' original register r
+template <Layout X, int L>
+__device__ __forceinline__ void derivative(S16 &s, uint32_t lane) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    uint32_t al = 0, ah = 0;
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      if (lane_pbit<X>(u) >= L) continue;  // an instance bit
+      const uint32_t m = ((lane >> u) & 1) ? 0u : 0xffffffffu;
+      al ^= from_upper(s.l[r], u) & m;
+      ah ^= from_upper(s.h[r], u) & m;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (reg_pbit<X>(t) < L && !(r & (1 << t))) {
+        al ^= s.l[r | (1 << t)];
+        ah ^= s.h[r | (1 << t)];
+      }
+    s.l[r] ^= al;
+    s.h[r] ^= ah;
+  }
+}
+
+
+// ---- FFT_n restricted to the outputs y < k = 2^KB (afft, additive_fft.hpp:121-141),
+// from the layout the derivative ran in (X = C for n >= 512, B below):
+//  * register-held stages t >= KB keep only the side that reaches y < k
+//    (a ^= b * s); registers with such a bit set are dead afterwards;
+//  * register-held stages below KB are full butterflies on the live registers;
+//  * the lane-held stages (p5..p0 in C, p3..p0 in B) run in registers after
+//    swapping each lane bit with register bit SB (the one of p6 / p4, whose
+//    stage is done) by DPP / v_permlane*_swap: no LDS exchange.
+// Afterwards: SB = p0, lane bits 0.. = p1.., the other register bits unchanged.
+template <Layout X>
+__host__ __device__ constexpr int rbit_of(int p) {
+  return reg_pbit<X>(0) == p ? 0 : reg_pbit<X>(1) == p ? 1 : reg_pbit<X>(2) == p ? 2
+                                 : reg_pbit<X>(3) == p ? 3 : -1;
+}
+// register r is still needed after the a-only stages above t (t = KB - 1: all)
+template <Layout X, int L, int KB>
+__host__ __device__ constexpr bool live_above(int r, int t) {
+  for (int p = (t + 1 > KB ? t + 1 : KB); p < L; ++p) {
+    const int b = rbit_of<X>(p);
+    if (b >= 0 && ((r >> b) & 1)) return false;
+  }
+  return true;
+}
+// local position bits held in register r (register bit skip excluded)
+template <Layout X, int L>
+__host__ __device__ constexpr uint32_t reg_pos(int r, int skip) {
+  uint32_t v = 0;
+  for (int b = 0; b < 4; ++b)
+    if (b != skip && ((r >> b) & 1) && reg_pbit<X>(b) < L) v |= 1u << reg_pbit<X>(b);
+  return v;
+}
+template <Layout X>
+__host__ __device__ constexpr int swap_rbit() { return X == LC ? 2 : 0; }  // p6 / p4
+template <Layout X>
+__host__ __device__ constexpr int lane_stages() { return X == LC ? 6 : 4; }  // p0..p5 / p0..p3
+
+// swap register bit (x: bit 0, y: bit 1) with lane bit b; hi = this lane's bit b
+__device__ __forceinline__ void swap_bit(uint32_t &x, uint32_t &y, int b, bool hi) {
+  if (b == 4) {
+    auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+    return;
+  }
+  if (b == 5) {
+    auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+    return;
+  }
+  const uint32_t send = hi ? x : y;  // lane bit 1 sends x, lane bit 0 sends y
+  uint32_t recv;
+  switch (b) {
+    case 0: recv = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0xB1, 0xf, 0xf, true)); break;  // quad [1,0,3,2]
+    case 1: recv = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x4E, 0xf, 0xf, true)); break;  // quad [2,3,0,1]
+    case 2: {
+      const uint32_t up = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x104, 0xf, 0xf, true));
+      const uint32_t dn = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x114, 0xf, 0xf, true));
+      recv = hi ? dn : up;
+      break;
+    }
+    default: recv = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x128, 0xf, 0xf, true)); break;  // row_ror:8
+  }
+  if (hi) x = recv;
+  else y = recv;
+}
+
+template <Layout X, int L, int KB>
+__device__ __forceinline__ void fft_restricted(S16 &s, const uint8_t *tabs, uint32_t lane) {
+  constexpr int F = X == LC ? 6 : 4;  // lowest register-held position bit
+  constexpr int SB = swap_rbit<X>(), NL = lane_stages<X>();
+  // register-held stages L-1 .. F (tables: wave-uniform, from the register bits above t)
+#pragma unroll
+  for (int t = L - 1; t >= F; --t) {
+    const int b = rbit_of<X>(t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (((r >> b) & 1) || !live_above<X, L, KB>(r, t)) continue;
+      Tab T;
+      tab_at(tabs, tlin(skew_idx(reg_pos<X, L>(r, -1), t)), T);
+      if (t >= KB) mul_acc(s.l[r | (1 << b)], s.h[r | (1 << b)], T, s.l[r], s.h[r]);  // a-side only
+      else fb(s, r, r | (1 << b), T);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // lane-held stages NL-1 .. 0: swap lane bit u into register bit SB, butterfly
+#pragma unroll
+  for (int u = NL - 1; u >= 0; --u) {
+    uint32_t l = lane;
+    asm volatile("" : "+v"(l));
+    const bool hi = (l >> u) & 1;
+    // bits above u now: p(u+1)..p(NL) in lane bits u..NL-1, the rest in registers
+    const uint32_t lane_hi = ((l & ((1u << NL) - 1)) >> u) << (u + 1);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (((r >> SB) & 1) || !live_above<X, L, KB>(r & ~(1 << SB), KB - 1)) continue;
+      const int r1 = r | (1 << SB);
+      swap_bit(s.l[r], s.l[r1], u, hi);
+      swap_bit(s.h[r], s.h[r1], u, hi);
+      Tab T;
+      tab_at(tabs, tlin(skew_idx((lane_hi | reg_pos<X, L>(r, SB)) & ((1u << L) - 1), u)), T);
+      fb(s, r, r1, T);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+
 // byte-planar group (4 pieces / columns) -> big-endian u16 x4
 __device__ __forceinline__ uint2 to_be(uint32_t l, uint32_t h) {
   return make_uint2(vperm(l, h, 0x05010400u), vperm(l, h, 0x07030602u));
