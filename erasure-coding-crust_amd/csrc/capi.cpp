@@ -64,7 +64,8 @@ bool encode_host(const CodeParams &p, const uint8_t *payload, size_t len, HostCt
       !ensure_host(&c->h_out, &c->h_out_cap, out_bytes) ||
       !ensure_dev(reinterpret_cast<void **>(&c->d_out), &c->d_out_cap, size_t(p.nv) * dstride))
     return false;
-  void *scratch = device_scratch(d, encode_scratch_bytes(p, len, 1));
+  ScratchLease lease(d, encode_scratch_bytes(p, len, 1), c->stream);
+  void *scratch = lease.ptr();
   std::memcpy(c->h_in, payload, len);
   if (!hip_check(hipMemcpyAsync(c->d_in, c->h_in, len, hipMemcpyHostToDevice, c->stream), "H2D") ||
       !hip_check(launch_encode(p, device_tables(d), c->d_in, len, len, 1, c->d_out, dstride,
@@ -107,7 +108,8 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
   } else {
     const uint16_t *fold = device_fold(d, p.n);
     if (!fold) return false;
-    void *scratch = device_scratch(d, reconstruct_scratch_bytes(p, sl, 1));
+    ScratchLease lease(d, reconstruct_scratch_bytes(p, sl, 1), c->stream);
+    void *scratch = lease.ptr();
     if (!hip_check(hipMemcpyAsync(c->d_present, present.data(), p.n, hipMemcpyHostToDevice,
                                   c->stream),
                    "H2D present") ||
@@ -355,7 +357,8 @@ NPRSResult ECCR_AMD_encode_batch(unsigned long nv, const uint8_t *d_payloads, un
   if (sstride < shard_len(p.k, plen) || pstride < plen) return result(NPRS_RESULT_BAD_PAYLOAD);
   DeviceState *d = device_state();
   if (!d) return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
-  void *scratch = device_scratch(d, encode_scratch_bytes(p, plen, batch));
+  ScratchLease lease(d, encode_scratch_bytes(p, plen, batch), static_cast<hipStream_t>(stream));
+  void *scratch = lease.ptr();
   if (!hip_check(launch_encode(p, device_tables(d), d_payloads, plen, pstride, batch, d_shards,
                                sstride, scratch, static_cast<hipStream_t>(stream)),
                  "encode launch"))
@@ -390,7 +393,8 @@ NPRSResult ECCR_AMD_reconstruct_batch(unsigned long nv, const uint8_t *d_shards,
   if (sstride < slen || ostride < slen * p.k) return result(NPRS_RESULT_NON_UNIFORM_CHUNKS);
   DeviceState *d = device_state();
   if (!d) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-  void *scratch = device_scratch(d, reconstruct_scratch_bytes(p, slen, batch));
+  ScratchLease lease(d, reconstruct_scratch_bytes(p, slen, batch), static_cast<hipStream_t>(stream));
+  void *scratch = lease.ptr();
   if (!hip_check(launch_reconstruct(p, device_tables(d), d_shards, slen, sstride, d_present,
                                     d_err_log, batch, d_out, ostride, scratch,
                                     static_cast<hipStream_t>(stream)),

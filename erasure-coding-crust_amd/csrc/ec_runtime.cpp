@@ -17,8 +17,11 @@ struct DeviceState {
   uint8_t *timg = nullptr;
   std::mutex mu;
   std::map<uint32_t, uint16_t *> fold;
+  std::mutex scratch_mu;  // held by a ScratchLease
   void *scratch = nullptr;
   size_t scratch_cap = 0;
+  hipEvent_t scratch_done = nullptr;  // the last lease's work on its stream
+  bool scratch_used = false;
 };
 
 namespace {
@@ -101,19 +104,31 @@ const uint16_t *device_fold(DeviceState *d, uint32_t n) {
   return p;
 }
 
-void *device_scratch(DeviceState *d, size_t bytes) {
-  if (bytes == 0) return nullptr;
-  std::lock_guard<std::mutex> lk(d->mu);
-  if (d->scratch_cap >= bytes) return d->scratch;
-  if (d->scratch) {
-    (void)hipDeviceSynchronize();
-    (void)hipFree(d->scratch);
+ScratchLease::ScratchLease(DeviceState *d, size_t bytes, hipStream_t stream)
+    : d_(d), s_(stream) {
+  if (!d || bytes == 0) return;
+  d->scratch_mu.lock();
+  held_ = true;
+  if (d->scratch_cap < bytes) {
+    if (d->scratch) {
+      if (d->scratch_used) (void)hipEventSynchronize(d->scratch_done);
+      (void)hipFree(d->scratch);
+    }
+    d->scratch = nullptr;
+    d->scratch_cap = 0;
+    if (!hip_ok(hipMalloc(&d->scratch, bytes), "hipMalloc(scratch)")) return;
+    d->scratch_cap = bytes;
+  } else if (d->scratch_used) {
+    (void)hipStreamWaitEvent(stream, d->scratch_done, 0);
   }
-  d->scratch = nullptr;
-  d->scratch_cap = 0;
-  if (!hip_ok(hipMalloc(&d->scratch, bytes), "hipMalloc(scratch)")) return nullptr;
-  d->scratch_cap = bytes;
-  return d->scratch;
+  p_ = d->scratch;
+}
+
+ScratchLease::~ScratchLease() {
+  if (!held_) return;
+  if (!d_->scratch_done) (void)hipEventCreateWithFlags(&d_->scratch_done, hipEventDisableTiming);
+  d_->scratch_used = d_->scratch_done && hipEventRecord(d_->scratch_done, s_) == hipSuccess;
+  d_->scratch_mu.unlock();
 }
 
 bool ensure_host(uint8_t **p, size_t *cap, size_t need) {

@@ -19,7 +19,25 @@ struct DeviceState;
 DeviceState *device_state();
 DevTables device_tables(DeviceState *d);
 const uint16_t *device_fold(DeviceState *d, uint32_t n);  // folded LOG_WALSH for n
-void *device_scratch(DeviceState *d, size_t bytes);       // grow-only, per device
+// Per-device scratch for the launches that need one (the k = 1024 encode's
+// coefficients between its four launches, generic kernels beyond LDS).  A
+// lease is held while a launch is enqueued: it orders the caller's stream
+// after the previous lease's work (an event), so launches from different
+// streams or host threads never overlap on the buffer.
+class ScratchLease {
+ public:
+  ScratchLease(DeviceState *d, size_t bytes, hipStream_t stream);
+  ~ScratchLease();  // records the release event on the stream
+  ScratchLease(const ScratchLease &) = delete;
+  ScratchLease &operator=(const ScratchLease &) = delete;
+  void *ptr() const { return p_; }
+
+ private:
+  DeviceState *d_ = nullptr;
+  hipStream_t s_ = nullptr;
+  void *p_ = nullptr;
+  bool held_ = false;
+};
 
 // Growable buffers of one host thread (reentrancy = the reference's
 // thread_local scratch, reed-solomon.hpp:198-201).

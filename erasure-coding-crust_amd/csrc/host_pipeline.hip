@@ -136,7 +136,8 @@ NPRSResult ECCR_AMD_encode_host_batch(unsigned long nv, const uint8_t *h_payload
     const size_t cb = batch - c0 < chunk ? batch - c0 : chunk;
     if (!grow(&s.d_a, &s.cap_a, chunk * dps) || !grow(&s.d_b, &s.cap_b, chunk * nv * dss))
       return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
-    void *scratch = device_scratch(d, encode_scratch_bytes(p, plen, cb));
+    ScratchLease lease(d, encode_scratch_bytes(p, plen, cb), s.stream);  // slots never share it concurrently
+    void *scratch = lease.ptr();
     const uint8_t *hp = h_payloads + c0 * pstride;
     uint8_t *hs = h_shards + c0 * nv * sstride;
     const hipError_t up =
@@ -207,7 +208,8 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
         !grow(&s.d_elog, &s.cap_elog, chunk * p.n * 2) ||
         !grow(&s.d_idx, &s.cap_idx, chunk * cnt * 2))
       return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-    void *scratch = device_scratch(d, reconstruct_scratch_bytes(p, slen, cb));
+    ScratchLease lease(d, reconstruct_scratch_bytes(p, slen, cb), s.stream);  // slots never share it concurrently
+    void *scratch = lease.ptr();
     bool good =
         ok(hipMemcpyAsync(s.d_a, h_shards + c0 * cnt * sstride, cb * cnt * sstride,
                           hipMemcpyHostToDevice, s.stream),

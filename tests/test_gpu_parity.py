@@ -209,14 +209,17 @@ def test_batch_systematic():
 
 # ---------------------------------------------------------------- host batches (row f2)
 @pytest.mark.parametrize("nv,plen,batch,chunk", [(1024, 70001, 7, 2), (100, 5000, 5, 0),
-                                                 (1024, 1_000_000, 4, 3)])
+                                                 (1024, 1_000_000, 4, 3),
+                                                 # k = 1024: chunks on the 3 slot streams
+                                                 # share the encode's coefficient scratch
+                                                 (4096, 60001, 7, 1)])
 def test_host_batch_roundtrip(oracle, nv, plen, batch, chunk):
     n, k, thr = E.code_params(nv)
     sl = E.shard_len(nv, plen)
     pay = np.stack([synth.payload(500 + b, plen) for b in range(batch)])
     sh = np.zeros((batch, nv, sl), dtype=np.uint8)
     E.encode_host_batch(nv, pay, plen, plen, batch, sh, sl, chunk)
-    for b in (0, batch - 1):
+    for b in range(batch):
         assert b"".join(oracle.encode(nv, pay[b].tobytes())) == sh[b].tobytes(), b
     cnt = thr
     idx = np.stack([np.sort(synth.present_set(700 + b, nv, cnt)) for b in range(batch)]).astype(np.uint16)
@@ -250,3 +253,41 @@ def test_encode_shard_base_8_aligned(oracle, nv):
     sh = d_sh.cpu().numpy().reshape(batch, nv, ss)[:, :, :sl]
     for b in range(batch):
         assert b"".join(oracle.encode(nv, pay[b, :plen].tobytes())) == sh[b].tobytes(), b
+
+
+def test_capi_concurrent_threads(oracle):
+    """The C ABI is reentrant like the reference (thread_local scratch,
+    reed-solomon.hpp:198-201): host threads encoding / reconstructing at once,
+    including k = 1024 encodes (the shared coefficient scratch), give the
+    single-threaded results."""
+    import threading
+    cases = [(4096, 30001), (4096, 50001), (1024, 40001), (600, 20001), (3070, 30001), (100, 9999)]
+    want = {}
+    for nv, plen in cases:
+        p = synth.payload(nv + plen, plen).tobytes()
+        want[(nv, plen)] = (p, b"".join(oracle.encode(nv, p)))
+    errors = []
+
+    def worker(tid):
+        try:
+            for rep in range(3):
+                nv, plen = cases[(tid + rep) % len(cases)]
+                p, ref = want[(nv, plen)]
+                sh = E.obtain_chunks(nv, p)
+                if b"".join(sh) != ref:
+                    errors.append(("encode", tid, nv))
+                    continue
+                n, k, thr = E.code_params(nv)
+                keep = set(int(x) for x in synth.present_set(tid * 7 + rep, nv, thr))
+                if decode_subset(nv, sh, keep)[:plen] != p:
+                    errors.append(("reconstruct", tid, nv))
+        except Exception as e:  # surfaced below
+            errors.append(("exception", tid, repr(e)))
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(6)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(120)
+    assert not any(t.is_alive() for t in threads)
+    assert not errors, errors
