@@ -51,14 +51,19 @@ bool hip_check(hipError_t e, const char *what) {
   return false;
 }
 
-// host -> device -> host encode of one payload into pinned h_out [nv][sl]
+// device row pitch of the per-call paths: 16-B aligned rows for the fast
+// kernels; the host staging buffers use the same pitch, so every host<->device
+// copy is one linear transfer (a 2-D copy of narrow rows costs ~10 us per row)
+inline size_t dev_pitch(size_t sl) { return (sl + 15) / 16 * 16; }
+
+// host -> device -> host encode of one payload into pinned h_out [nv][dev_pitch(sl)]
 bool encode_host(const CodeParams &p, const uint8_t *payload, size_t len, HostCtx *c,
                  size_t *sl_out) {
   DeviceState *d = device_state();
   if (!d) return false;
   const size_t sl = shard_len(p.k, len);
-  const size_t dstride = (sl + 15) / 16 * 16;  // aligned device rows for the fast kernels
-  const size_t out_bytes = size_t(p.nv) * sl;
+  const size_t dstride = dev_pitch(sl);
+  const size_t out_bytes = size_t(p.nv) * dstride;
   if (!ensure_host(&c->h_in, &c->h_in_cap, len) ||
       !ensure_dev(reinterpret_cast<void **>(&c->d_in), &c->d_in_cap, len) ||
       !ensure_host(&c->h_out, &c->h_out_cap, out_bytes) ||
@@ -71,8 +76,7 @@ bool encode_host(const CodeParams &p, const uint8_t *payload, size_t len, HostCt
       !hip_check(launch_encode(p, device_tables(d), c->d_in, len, len, 1, c->d_out, dstride,
                                scratch, c->stream),
                  "encode launch") ||
-      !hip_check(hipMemcpy2DAsync(c->h_out, sl, c->d_out, dstride, sl, p.nv,
-                                  hipMemcpyDeviceToHost, c->stream),
+      !hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost, c->stream),
                  "D2H") ||
       !hip_check(hipStreamSynchronize(c->stream), "encode"))
     return false;
@@ -80,13 +84,13 @@ bool encode_host(const CodeParams &p, const uint8_t *payload, size_t len, HostCt
   return true;
 }
 
-// reconstruct from shards staged in c->h_in ([nv][sl], present[] flags) into c->h_out
+// reconstruct from shards staged in c->h_in ([nv][dev_pitch(sl)], present[] flags) into c->h_out
 bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, size_t sl,
                       HostCtx *c) {
   DeviceState *d = device_state();
   if (!d) return false;
   const size_t in_bytes = size_t(p.nv) * sl, out_bytes = sl * p.k;
-  const size_t dstride = (sl + 15) / 16 * 16;  // aligned device rows for the fast kernels
+  const size_t dstride = dev_pitch(sl);
   if (!ensure_dev(reinterpret_cast<void **>(&c->d_in), &c->d_in_cap, size_t(p.nv) * dstride) ||
       !ensure_dev(reinterpret_cast<void **>(&c->d_out), &c->d_out_cap, out_bytes) ||
       !ensure_host(&c->h_out, &c->h_out_cap, out_bytes) ||
@@ -96,8 +100,8 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
   bool all_systematic = true;
   for (uint32_t y = 0; y < p.k; ++y) all_systematic &= present[y] != 0;
   (void)in_bytes;
-  if (!hip_check(hipMemcpy2DAsync(c->d_in, dstride, c->h_in, sl, sl, p.nv, hipMemcpyHostToDevice,
-                                  c->stream),
+  if (!hip_check(hipMemcpyAsync(c->d_in, c->h_in, size_t(p.nv) * dstride, hipMemcpyHostToDevice,
+                                c->stream),
                  "H2D"))
     return false;
   if (all_systematic) {
@@ -187,7 +191,7 @@ NPRSResult ECCR_obtain_chunks(unsigned long nv, const DataBlock *message, Chunks
   if (!chunks) return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
   for (unsigned long v = 0; v < nv; ++v) {
     uint8_t *b = static_cast<uint8_t *>(std::malloc(sl));
-    std::memcpy(b, c->h_out + v * sl, sl);
+    std::memcpy(b, c->h_out + v * dev_pitch(sl), sl);
     chunks[v].data.array = b;
     chunks[v].data.length = sl;
     chunks[v].index = v;
@@ -233,10 +237,10 @@ NPRSResult ECCR_reconstruct(unsigned long nv, const ChunksList *input, DataBlock
     }
   if (count < p.k) return result(NPRS_RESULT_NOT_ENOUGH_CHUNKS);  // reed-solomon.hpp:99-100
   HostCtx *c = host_ctx();
-  if (!c || !ensure_host(&c->h_in, &c->h_in_cap, size_t(nv) * sl))
+  if (!c || !ensure_host(&c->h_in, &c->h_in_cap, size_t(nv) * dev_pitch(sl)))
     return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
   for (unsigned long v = 0; v < nv; ++v)
-    if (slot[v]) std::memcpy(c->h_in + v * sl, slot[v]->data.array, sl);
+    if (slot[v]) std::memcpy(c->h_in + v * dev_pitch(sl), slot[v]->data.array, sl);
   if (!reconstruct_host(p, present, sl, c) || !take_output(c, sl * p.k, outdata))
     return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
   return result(NPRS_RESULT_OK);
@@ -303,9 +307,9 @@ NPRSResult ECCR_Test_MeasurePerformance(const DataBlock *message, unsigned long 
     return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
   const auto t1 = clk::now();
   // reconstruct from all shards (src/erasure_coding.rs:200-211)
-  if (!ensure_host(&c->h_in, &c->h_in_cap, size_t(nv) * sl))
+  if (!ensure_host(&c->h_in, &c->h_in_cap, size_t(nv) * dev_pitch(sl)))
     return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-  std::memcpy(c->h_in, c->h_out, size_t(nv) * sl);
+  std::memcpy(c->h_in, c->h_out, size_t(nv) * dev_pitch(sl));
   std::vector<uint8_t> present(p.n, 0);
   for (unsigned long v = 0; v < nv; ++v) present[v] = 1;
   const auto t2 = clk::now();
