@@ -68,11 +68,6 @@ __device__ __forceinline__ uint32_t raddr(uint32_t v) {
   return ((v >> 5) << 8) | (f << 3);
 }
 
-__device__ __forceinline__ void lds_tab(const uint8_t *base, uint32_t idx, Tab &T) {
-  if ((DEC_ABL & 32) && idx > 7) return;
-  Tabs::load(base, idx, T);
-}
-
 __device__ __forceinline__ uint32_t skew_idx(uint32_t pos_a, int m) {
   const uint32_t d = 1u << m;
   return (pos_a & ~(2 * d - 1)) + d - 1;  // FFT index 0 (poly_encoder.hpp:180,183)

@@ -225,7 +225,6 @@ __device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t b
 // layout C: register bit0 = p6, bit1 = p7, bit2 = p5 (passenger); stages 6, 7
 // have lane-uniform skews.
 __device__ __forceinline__ void ipassC(State &s, const uint8_t *tabs, uint32_t off) {
-  bool first = true;
   Tab Ta, Tb;
   lds_tab_at(tabs, tlin(skew_idx(0, 6, off)), Ta);
   lds_tab_at(tabs, tlin(skew_idx(1u << 7, 6, off)), Tb);
@@ -241,7 +240,6 @@ __device__ __forceinline__ void ipassC(State &s, const uint8_t *tabs, uint32_t o
 }
 
 __device__ __forceinline__ void fpassC(State &s, const uint8_t *tabs, uint32_t off) {
-  bool first = true;
   Tab Ta, Tb;
   lds_tab_at(tabs, tlin(skew_idx(0, 7, off)), Ta);
   lds_tab_at(tabs, tlin(skew_idx(0, 6, off)), Tb);
@@ -261,14 +259,14 @@ __device__ __forceinline__ uint32_t posA(uint32_t q, int r) { return (q << 3) | 
 __device__ __forceinline__ uint32_t posB(uint32_t q, int r) {
   return ((q >> 3) << 6) | (uint32_t(r) << 3) | (q & 7);
 }
-__device__ __forceinline__ uint32_t posC(uint32_t q, int r) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t posC(uint32_t q, int r) {
   return (uint32_t(r & 3) << 6) | (uint32_t(r >> 2) << 5) | q;
 }
 
 // ---- wave-private exchange -------------------------------------------------
 // GP = 2: 16-byte cell (pos, inst) = both groups; 256-byte windows of 8 positions
 // with the cell XOR-swizzled by h(window) (layout A/B/C reads conflict-free).
-__device__ __forceinline__ uint32_t xaddr16(uint32_t pos, uint32_t inst) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t xaddr16(uint32_t pos, uint32_t inst) {
   const uint32_t w = pos >> 3;
   const uint32_t h = (w & 15) ^ ((w >> 3) & 1);
   return (w << 8) | ((((pos & 7) * 2 + inst) ^ h) << 4);
@@ -359,7 +357,7 @@ __device__ __forceinline__ uint2 to_be(uint32_t l, uint32_t h) {
 }
 
 // registers in layout A -> LDS staging rows 0..255 (shard = s0 + row)
-__device__ __forceinline__ void stage_rows(const State &s, uint8_t *stg, uint32_t q, uint32_t inst,
+[[maybe_unused]] __device__ __forceinline__ void stage_rows(const State &s, uint8_t *stg, uint32_t q, uint32_t inst,
                                            uint32_t wave) {
   if (ENC_ABL & 8) return;
 #pragma unroll
@@ -373,7 +371,7 @@ __device__ __forceinline__ void stage_rows(const State &s, uint8_t *stg, uint32_
 }
 
 // all waves: LDS rows -> shards [s0, s0+256), 256-byte row segments
-__device__ __forceinline__ void store_rows(const uint8_t *stg, uint8_t *SH, uint64_t sstride,
+[[maybe_unused]] __device__ __forceinline__ void store_rows(const uint8_t *stg, uint8_t *SH, uint64_t sstride,
                                            uint32_t s0, int nv, uint64_t piece0, uint64_t npieces,
                                            uint32_t wave, uint32_t lane) {
   if (ENC_ABL & 9) return;
@@ -406,7 +404,7 @@ __device__ __forceinline__ uint32_t saddr16(uint32_t v, uint32_t slot16) {
   return v * 256 + ((slot16 ^ ((v >> 3) & 15)) << 4);
 }
 
-__device__ __forceinline__ void stage_rows16(const State &s, uint8_t *stg, uint32_t q,
+[[maybe_unused]] __device__ __forceinline__ void stage_rows16(const State &s, uint8_t *stg, uint32_t q,
                                              uint32_t inst, uint32_t wave) {
 #pragma unroll
   for (int r = 0; r < 8; ++r)
@@ -416,7 +414,7 @@ __device__ __forceinline__ void stage_rows16(const State &s, uint8_t *stg, uint3
 
 // all waves: LDS rows -> shards [s0, s0 + 256); lane = (row-in-4, 16-B chunk),
 // one dwordx4 per lane per row: 4 store instructions per wave per shift.
-__device__ __forceinline__ void store_rows16(const uint8_t *stg, uint8_t *SH, uint64_t sstride,
+[[maybe_unused]] __device__ __forceinline__ void store_rows16(const uint8_t *stg, uint8_t *SH, uint64_t sstride,
                                              uint32_t s0, int nv, uint64_t piece0,
                                              uint64_t npieces, uint32_t wave, uint32_t lane) {
   const uint32_t c = lane & 15;
@@ -497,7 +495,7 @@ __device__ __forceinline__ void store_own(const uint8_t *xbase, uint8_t *SH, uin
 // registers in layout A -> shards [s0 + 8q, s0 + 8q + 8) straight from the
 // registers: lanes (q, 0) and (q, 1) write 16 contiguous bytes of a row; the
 // L2 merges the 16 waves' pieces into full lines.  No staging, no barriers.
-__device__ __forceinline__ void store_direct(const State &s, uint8_t *SH, uint64_t sstride,
+[[maybe_unused]] __device__ __forceinline__ void store_direct(const State &s, uint8_t *SH, uint64_t sstride,
                                              uint32_t s0, int nv, uint64_t piece0,
                                              uint64_t npieces, uint32_t q, uint32_t inst,
                                              uint32_t wave) {
