@@ -223,12 +223,15 @@ __global__ void __launch_bounds__(THREADS)
       }
     }
 
-    // ---- systematic shards 0..k-1 = the data symbols (poly_encoder.hpp:239)
+    // ---- systematic shards 0..k-1 = the data symbols (poly_encoder.hpp:239).
+    // Barriers are lazy: a wave's region is next written by its first exchange
+    // (or staging), so the barrier that waits for the other waves' reads of
+    // the regions (store_rows) sits right before that write, and the stores
+    // overlap the register-only first pass that precedes it.
     lds_barrier();  // the other waves are done reading the regions (last tile)
     stage<M>(s, my, lane);
     lds_barrier();
     store_rows<M>(regions, SH, sstride, 0, nv, piece0, npieces, tid);
-    lds_barrier();
 
     // ---- IFFT_k (index 0): pass A, exchange, pass B -> layout B
     if (img != 0) {  // the previous tile ended on a higher image
@@ -240,9 +243,11 @@ __global__ void __launch_bounds__(THREADS)
     if constexpr (M == 4) {
       // k = 16: the whole IFFT is pass A; coefficients stay in layout A
     } else if constexpr (M <= 8) {
+      lds_barrier();  // systematic rows read out of the regions
       exchange<LA, LB>(s, my, lane);
       ipassg<4, M - 4, M>(s, tabs, 0);
     } else {
+      lds_barrier();  // systematic rows read out of the regions
       exchange<LA, LB>(s, my, lane);
       ipassg<4, 4, M>(s, tabs, lbB(lane));
       exchange<LB, LC>(s, my, lane);
@@ -252,7 +257,7 @@ __global__ void __launch_bounds__(THREADS)
 
     // ---- FFT_k at each coset shift (encodeLow, poly_encoder.hpp:229-237)
     for (int sh = int(Gm::K); sh < n && sh < nv; sh += int(Gm::K)) {
-      if ((sh >> 10) != img) {  // every wave is past the last barrier of the previous coset
+      if ((sh >> 10) != img) {  // (load_image waits for every wave's last table reads)
         img = sh >> 10;
         load_image(img);
       }
@@ -261,21 +266,22 @@ __global__ void __launch_bounds__(THREADS)
       for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(s.l[r]), "+v"(s.h[r]));
       const uint32_t lo = tlin(uint32_t(sh) & 1023u);  // tables at offset sh (disjoint bits)
       if constexpr (M == 4) {
+        lds_barrier();  // previous rows read out of the regions
       } else if constexpr (M <= 8) {
         fpassg<4, M - 4, M>(s, tabs, lo);
+        lds_barrier();  // previous rows read out of the regions
         exchange<LB, LA>(s, my, lane);
       } else {
         fpassC9(s, tabs, lo);
+        lds_barrier();  // previous rows read out of the regions
         exchange<LC, LB>(s, my, lane);
         fpassg<4, 4, M>(s, tabs, lbB(lane) ^ lo);
         exchange<LB, LA>(s, my, lane);
       }
       fpassg<0, (M < 4 ? M : 4), M>(s, tabs, tlin((16 * lane) & (Gm::K - 1)) ^ lo);
-      lds_barrier();  // all waves done with their regions (exchange, previous stores)
-      stage<M>(s, my, lane);
+      stage<M>(s, my, lane);  // own region: no other wave touches it since the barrier above
       lds_barrier();
       store_rows<M>(regions, SH, sstride, uint32_t(sh), nv, piece0, npieces, tid);
-      lds_barrier();
     }
   }
 }
