@@ -32,7 +32,6 @@ namespace ecamd {
 namespace {
 
 constexpr int K = 256;
-constexpr int N = 1024;
 // GP byte-planar groups per lane (registers), WAVES per workgroup.  GP = 1 with
 // 16 waves gives 4 waves/SIMD (<= 128 VGPRs) for latency hiding; the tile is
 // 128 pieces either way.
@@ -528,6 +527,10 @@ __device__ __forceinline__ void store_own(const uint8_t *xbase, uint8_t *SH, uin
 
 }  // namespace
 
+// N = n: 1024 (n_validators 766..1024) or 2048 (1025..1533); the cosets at
+// 1024 and above use LDS table image 1 (skews 1024 .. 2046, DevTables::timg)
+// at offset sh - 1024, reloaded by LDS-DMA between the two coset loops
+template <int N>
 __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict__ payloads,
                                                        uint64_t plen, uint64_t pstride,
                                                        uint8_t *__restrict__ shards, uint64_t slen,
@@ -541,6 +544,13 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
   // resident multiply tables for skew indices 0..1022 (all FFTs of k=256, n=1024)
   Tabs::fill(tabs, t.mtab, 1023, [&](uint32_t i) { return uint32_t(t.skews[i]); }, tid0, THREADS);
   __syncthreads();
+  [[maybe_unused]] int img = 0;
+  [[maybe_unused]] const auto load_image = [&](int q) {  // LDS-DMA: no VGPRs (the kernel is at 128)
+    lds_barrier();  // every wave is done with the current tables
+    Tabs::dma_image<THREADS>(tabs, t.timg + q * kTabImageBytes, tid0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+  };
 
   const uint64_t npieces = slen / 2;
   const uint32_t tiles_pp = uint32_t((npieces + TILE - 1) / TILE);
@@ -613,6 +623,12 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     }
 
     // ---- IFFT_256 (index 0): passes A (bits 0-2), B (3-5), C (6-7)
+    if constexpr (N > 1024) {
+      if (img != 0) {  // the previous tile ended on image 1
+        load_image(0);
+        img = 0;
+      }
+    }
     ipass3(s, tabs, posA(q, 0), 0, 0);
     if constexpr (kOwn) lds_barrier();  // systematic rows read out of the regions
     exchange<LA, LB>(s, xch, xb, q, inst);
@@ -622,7 +638,7 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     const State coef = s;
 
     // ---- FFT_256 at each coset shift (encodeLow, poly_encoder.hpp:229-237)
-    for (uint32_t sh = K; sh < uint32_t(N) && int(sh) < nv; sh += K) {
+    const auto coset = [&](const uint32_t sh, const uint32_t off) __attribute__((always_inline)) {
       s = coef;
       // opaque copy: keeps the compiler from hoisting the first stage's selector
       // masks out of the coset loop (that costs ~50 VGPRs and forces spills)
@@ -630,12 +646,12 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
       for (int g = 0; g < GP; ++g)
 #pragma unroll
         for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(s.l[g][r]), "+v"(s.h[g][r]));
-      fpassC(s, tabs, sh);
+      fpassC(s, tabs, off);
       if (kOwn) lds_barrier();  // previous coset's rows read out
       exchange<LC, LB>(s, xch, xb, q, inst);
-      fpass3(s, tabs, posB(q, 0), 3, sh);
+      fpass3(s, tabs, posB(q, 0), 3, off);
       exchange<LB, LA>(s, xch, xb, q, inst);
-      fpass3(s, tabs, posA(q, 0), 0, sh);
+      fpass3(s, tabs, posA(q, 0), 0, off);
       if constexpr (kOwn) {
         stage_own(s, xch, q, inst, wave);
         lds_barrier();
@@ -650,11 +666,22 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
         STORE(stg, SH, sstride, sh, nv, piece0, npieces, wave, lane);
         lds_barrier();
       }
+        };
+    if constexpr (N == 1024) {
+      for (uint32_t sh = K; sh < 1024u && int(sh) < nv; sh += K) coset(sh, sh);
+    } else {
+      for (uint32_t sh = K; sh < uint32_t(N) && int(sh) < nv; sh += K) {
+        if (sh == 1024u) {
+          load_image(1);
+          img = 1;
+        }
+        coset(sh, sh & 1023u);
+      }
     }
   }
 }
 
-bool k256_applicable(const CodeParams &p) { return p.k == 256 && p.n == 1024; }
+bool k256_applicable(const CodeParams &p) { return p.k == 256 && (p.n == 1024 || p.n == 2048); }
 
 hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
@@ -665,16 +692,24 @@ hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uin
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&encode_k256),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&encode_k256<1024>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&encode_k256<2048>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return e;
   }
   const size_t sl = shard_len(p.k, plen);
   const size_t tiles = (sl / 2 + TILE - 1) / TILE * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
-  hipLaunchKernelGGL(encode_k256, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
-                     uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride),
-                     int(p.nv), uint32_t(batch), t);
+  if (p.n == 1024)
+    hipLaunchKernelGGL(encode_k256<1024>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
+                       uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl),
+                       uint64_t(sstride), int(p.nv), uint32_t(batch), t);
+  else
+    hipLaunchKernelGGL(encode_k256<2048>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
+                       uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl),
+                       uint64_t(sstride), int(p.nv), uint32_t(batch), t);
   return hipGetLastError();
 }
 
