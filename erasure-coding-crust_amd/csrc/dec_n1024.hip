@@ -194,44 +194,16 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   uint64_t st_ = __builtin_amdgcn_s_memtime(), acc_[11] = {};
 #endif
 
-  // a contiguous range of tiles per workgroup: consecutive tiles share a
-  // payload, so the locator-derived indices (this thread's two received rows
-  // and its share of the output-table fill) are loaded once per payload and
-  // each tile's table loads depend on no other global load
   const uint64_t ncols = slen / 2;
   const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);
   const uint64_t total = uint64_t(tiles_pp) * batch;
-  const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
-  const uint64_t tile_end = per * (blockIdx.x + 1) < total ? per * (blockIdx.x + 1) : total;
-  constexpr int FILL = (K * 5 + THREADS - 1) / THREADS;  // output-table chunks per thread
-  static_assert(FILL == 3, "index packing");
-  uint64_t cur_b = ~0ull;
-  // 16-bit packed: rows (0xffff = absent) and fill chunks (VGPRs are at the limit)
-  uint32_t rpack = 0, fpack01 = 0, fpack2 = 0;
-  for (uint64_t tile = per * blockIdx.x; tile < tile_end; ++tile) {
+  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
     const uint64_t b = tile / tiles_pp;
     const uint64_t col0 = (tile % tiles_pp) * COLS;
     const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
     const uint8_t *pr = present + b * N;
     const uint16_t *E = elog + b * N;
     uint8_t *O = out + b * ostride;
-    if (b != cur_b) {  // new payload (uniform)
-      cur_b = b;
-      uint32_t ri[2], fi[FILL];
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const uint32_t v = tid + half * THREADS;
-        ri[half] = (int(v) < nv && pr[v]) ? mul_index(E[v]) : 0xffffu;
-      }
-#pragma unroll
-      for (int it = 0; it < FILL; ++it) {
-        const uint32_t i = tid + it * THREADS;
-        fi[it] = i < uint32_t(K) * 5 ? mul_index(E[i / 5]) : 0u;
-      }
-      rpack = ri[0] | (ri[1] << 16);
-      fpack01 = fi[0] | (fi[1] << 16);
-      fpack2 = fi[2];
-    }
 
     // ---- phase 1: gather + scale rows v = tid, tid + 512 (decode_main:174-177)
     STAMP(0);
@@ -243,8 +215,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       uint32_t l[8], h[8];
 #pragma unroll
       for (int g = 0; g < 8; ++g) l[g] = h[g] = 0;
-      const uint32_t ridx = (rpack >> (16 * half)) & 0xffffu;
-      if (ridx != 0xffffu) {
+      if (int(v) < nv && pr[v]) {
         const uint8_t *row = SH + uint64_t(v) * sstride + 2 * col0;
         uint32_t w[16];
         const uint64_t avail = slen - 2 * col0;  // bytes of this row inside the tile
@@ -269,7 +240,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         }
         Tab T;
         if (DEC_ABL & 2) Tabs::load(tabs, v & 1023, T);
-        else load_tab(t.mtab, ridx, T);
+        else load_tab(t.mtab, mul_index(E[v]), T);
 #pragma unroll
         for (int g = 0; g < 8; ++g) {  // columns 4g..4g+3: words (h0 l0 h1 l1)(h2 l2 h3 l3)
           const uint32_t a = w[2 * g], c = w[2 * g + 1];
@@ -389,18 +360,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     }
     STAMP(6);
     __syncthreads();  // every wave is done with its region: reuse them for E[y] tables
-#pragma unroll
-    for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(ql[q]), "+v"(qh[q]));  // computed before the fill
-    if (!(DEC_ABL & 16)) {
-#pragma unroll
-      for (int it = 0; it < FILL; ++it) {
-        const uint32_t i = tid + it * THREADS;
-        if (i < uint32_t(K) * 5)
-          *reinterpret_cast<uint4 *>(regions + OutTabs::addr(i / 5, i % 5)) =
-              reinterpret_cast<const uint4 *>(
-                  t.mtab + (it == 2 ? fpack2 : (fpack01 >> (16 * it)) & 0xffffu))[i % 5];
-      }
-    }
+    if (!(DEC_ABL & 16))
+      OutTabs::fill(regions, t.mtab, K, [&](uint32_t y) { return mul_index(E[y]); }, tid, THREADS);
     STAMP(7);
     {
       // q bit0 = p6, bit1 = p7; lane bits = p0..p5.  Positions < 256 only.

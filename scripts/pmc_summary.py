@@ -40,7 +40,7 @@ def per_launch(path, counter):
     out = collections.defaultdict(list)
     for d, v in val.items():
         for k, short in KERNELS.items():
-            if k + "(" in name[d]:
+            if k + "(" in name[d] or k + "<" in name[d]:
                 out[short].append(v * 1024.0)
     return {k: sum(v) / len(v) for k, v in out.items()}
 
