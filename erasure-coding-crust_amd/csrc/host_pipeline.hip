@@ -59,6 +59,18 @@ struct Pipeline {
   int device = -1;
 };
 
+// chunk = 0: payloads per pipeline step such that a step moves ~16 MB over
+// the link (small payloads: few large copies instead of many latency-bound
+// ones; large payloads: still >= 3 steps in flight when the batch allows)
+unsigned long auto_chunk(size_t bytes_per_payload, unsigned long batch) {
+  const size_t target = size_t(16) << 20;
+  size_t c = bytes_per_payload ? target / bytes_per_payload : batch;
+  if (c < 1) c = 1;
+  if (batch >= 3 && c > (batch + 2) / 3 && bytes_per_payload * ((batch + 2) / 3) >= (size_t(4) << 20))
+    c = (batch + 2) / 3;  // keep the three slots busy on big batches
+  return c > batch ? batch : c;
+}
+
 Pipeline *pipeline() {  // one per host thread (reentrant like the reference)
   thread_local Pipeline pl;
   int dev = 0;
@@ -122,7 +134,7 @@ NPRSResult ECCR_AMD_encode_host_batch(unsigned long nv, const uint8_t *h_payload
   DeviceState *d = device_state();
   Pipeline *pl = d ? pipeline() : nullptr;
   if (!pl) return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
-  if (chunk == 0) chunk = 64;
+  if (chunk == 0) chunk = auto_chunk(plen + size_t(nv) * sl, batch);
   // Device rows use the host stride (one linear copy) when it already suits the
   // fast kernels or rows are short: a 2-D copy of many narrow rows is
   // descriptor-bound (2-byte rows ran at ~10 us per row).  Otherwise rows are
@@ -196,7 +208,7 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
   const uint16_t *fold = d ? device_fold(d, p.n) : nullptr;
   Pipeline *pl = fold ? pipeline() : nullptr;
   if (!pl) return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-  if (chunk == 0) chunk = 64;
+  if (chunk == 0) chunk = auto_chunk(size_t(cnt) * sstride + size_t(slen) * p.k, batch);
   const size_t dss = (slen + 63) / 64 * 64, ob = slen * p.k;
   const bool out_lin = ostride % 8 == 0 || ob < 256;  // as in encode: linear copy if it suits
   const size_t dos = out_lin ? ostride : ob;

@@ -73,7 +73,8 @@ struct NPRSResult ECCR_AMD_systematic_batch(unsigned long n_validators, const ui
 /* Last error message of the calling thread ("" if none). */
 /* ---- host-resident batches --------------------------
  * Stream a host batch through the device in chunks of `chunk` payloads (0 =
- * 64), three chunks in flight (H2D / kernels / D2H overlap).  Synchronous:
+ * automatic: ~16 MB over the link per chunk), three chunks in flight (H2D /
+ * kernels / D2H overlap).  Synchronous:
  * returns when the output is in host memory.  Host buffers should come from
  * ECCR_AMD_host_alloc (pinned) for full PCIe rate. */
 void *ECCR_AMD_host_alloc(unsigned long bytes);

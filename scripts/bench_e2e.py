@@ -9,7 +9,8 @@ must also be measured".  Not the bench.py `value` (that one is device-resident).
   C ABI per call         : ECCR_obtain_chunks / ECCR_reconstruct (pageable
                            buffers, per-shard malloc, as a reference caller)
   mixed stream           : README sizes {15 B .. 10 MB} through the host-batch
-                           API, one batch per size class (config 5 shape, 1 GPU)
+                           API, one batch per size class, automatic chunking
+                           (config 5 shape, 1 GPU)
 Prints one JSON object.
 """
 from __future__ import annotations
@@ -98,7 +99,7 @@ def main():
     mixed = []
     for plen, batch in ((15, 4096), (300, 4096), (5000, 2048), (100000, 512), (1_000_000, 128),
                         (10_000_000, 16)):
-        mixed.append(host_batch(a.nv, plen, batch, min(a.chunk, batch), 2))
+        mixed.append(host_batch(a.nv, plen, batch, 0, 2))  # chunk 0: library sizes the steps
     res["mixed_stream"] = mixed
     tot_b = sum(m["payload_bytes"] * m["batch"] for m in mixed)
     tot_t = sum(m["encode_s"] + m["reconstruct_s"] for m in mixed)
