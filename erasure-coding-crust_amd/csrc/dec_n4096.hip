@@ -182,7 +182,6 @@ reconstruct_n4096(
       load_tab(t.mtab, ik, TK);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        if (q == NQ - 1) P.l[r] = P.h[r] = Qa.l[r] = Qa.h[r] = 0;
         mul_acc(Qq.l[r], Qq.h[r], TP, P.l[r], P.h[r]);
         mul_acc(Qq.l[r], Qq.h[r], TK, Qa.l[r], Qa.h[r]);  // shares the selectors of the line above
       }
@@ -191,8 +190,12 @@ reconstruct_n4096(
         asm volatile("" : "+v"(P.l[r]), "+v"(P.h[r]), "+v"(Qa.l[r]), "+v"(Qa.h[r]));
       __builtin_amdgcn_sched_barrier(0);
     };
+#pragma unroll
+    for (int r = 0; r < 16; ++r) P.l[r] = P.h[r] = Qa.l[r] = Qa.h[r] = 0;
+    // a quarter wholly at or above n_validators holds no received symbol: its
+    // IFFT is zero and adds nothing (n = 4096 with n_validators <= 3072)
     if constexpr (NQ == 4) {
-      quarter(3);
+      if (3 * 1024 < nv) quarter(3);
       quarter(2);
     }
     quarter(1);
