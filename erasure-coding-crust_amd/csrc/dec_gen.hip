@@ -32,7 +32,7 @@ static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 
 __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ? 0u : c; }
 
-// inverse / forward pass over register bits 0..NS-1 (position bits B0..) of
+// inverse pass over register bits 0..NS-1 (position bits B0..) of
 // the local index pos & (n - 1); lb = tlin of the (masked) lane part
 template <int B0, int NS, int L>
 __device__ __forceinline__ void ipassg(S16 &s, const uint8_t *tabs, uint32_t lb) {
@@ -50,26 +50,6 @@ __device__ __forceinline__ void ipassg(S16 &s, const uint8_t *tabs, uint32_t lb)
         tab_at(tabs, lb ^ tlin(skew_idx((uint32_t(nblk) << B0) & NM, B0 + nt)), T[(k + 1) & 1]);
 #pragma unroll
       for (int i = 0; i < d; ++i) ib(s, blk + i, blk + i + d, T[k & 1]);
-    }
-  }
-}
-
-template <int B0, int NS, int L>
-__device__ __forceinline__ void fpassg(S16 &s, const uint8_t *tabs, uint32_t lb) {
-  constexpr uint32_t NM = (1u << L) - 1;
-  Tab T[2];
-  tab_at(tabs, lb ^ tlin(skew_idx(0, B0 + NS - 1)), T[0]);
-  int k = 0;
-#pragma unroll
-  for (int t = NS - 1; t >= 0; --t) {
-    const int d = 1 << t;
-#pragma unroll
-    for (int blk = 0; blk < 16; blk += 2 * d, ++k) {
-      const int nt = blk + 2 * d < 16 ? t : t - 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
-      if (nt >= 0)
-        tab_at(tabs, lb ^ tlin(skew_idx((uint32_t(nblk) << B0) & NM, B0 + nt)), T[(k + 1) & 1]);
-#pragma unroll
-      for (int i = 0; i < d; ++i) fb(s, blk + i, blk + i + d, T[k & 1]);
     }
   }
 }
@@ -95,25 +75,6 @@ __device__ __forceinline__ void ipassCg(S16 &s, const uint8_t *tabs) {
   }
 }
 
-template <int L>
-__device__ __forceinline__ void fpassCg(S16 &s, const uint8_t *tabs) {
-  constexpr uint32_t NM = (1u << L) - 1;
-  Tab Ta, Tb;
-  if constexpr (L == 10) {
-    tab_at(tabs, tlin(skew_idx(0, 9)), Ta);
-#pragma unroll
-    for (int hi = 0; hi < 4; ++hi) {
-      fb(s, 4 * hi, 4 * hi + 2, Ta);
-      fb(s, 4 * hi + 1, 4 * hi + 3, Ta);
-    }
-  }
-  tab_at(tabs, tlin(skew_idx(0, 8)), Ta);
-  tab_at(tabs, tlin(skew_idx((1u << 9) & NM, 8)), Tb);
-#pragma unroll
-  for (int hi = 0; hi < 4; ++hi) fb(s, 4 * hi, 4 * hi + 1, Ta);
-#pragma unroll
-  for (int hi = 0; hi < 4; ++hi) fb(s, 4 * hi + 2, 4 * hi + 3, Tb);
-}
 
 template <int L, int KB>
 __global__ void __launch_bounds__(THREADS) reconstruct_gen(
