@@ -111,6 +111,10 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
   uint64_t cur_b = ~0ull;
   Tab RT[RPT];  // E[v] tables of this thread's received rows
   bool rhave[RPT];
+  // the next tile's received rows are requested at the end of each gather and
+  // land during the transform (same payload and a whole tile only)
+  uint4 pre[CPT];
+  bool pre_ok = false;
   for (uint64_t tile = per * blockIdx.x; tile < tile_end; ++tile) {
     uint32_t tid = tid0;
     asm volatile("" : "+v"(tid));
@@ -153,7 +157,10 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
         for (int j = 0; j < JPR; ++j) {
           const uint32_t c16 = ch0 % CPR + j;
           uint32_t w[4] = {0, 0, 0, 0};
-          if (have) {
+          if (have && pre_ok) {
+            const uint4 d = pre[rr * JPR + j];
+            w[0] = d.x; w[1] = d.y; w[2] = d.z; w[3] = d.w;
+          } else if (have) {
             const uint8_t *src = SH + uint64_t(v) * sstride + 2 * col0 + 16 * c16;
             if (16 * (c16 + 1) <= avail) {
               const uint4 d = *reinterpret_cast<const uint4 *>(src);
@@ -172,6 +179,20 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
             *reinterpret_cast<uint2 *>(regions + gw * REG_BYTES + raddr((gi << L) | v)) =
                 make_uint2(l, h);
           }
+        }
+      }
+      // prefetch the next tile's rows (uniform condition)
+      const uint64_t nt = tile + 1, ncol0 = (nt % tiles_pp) * TC;
+      pre_ok = nt < tile_end && nt / tiles_pp == b && 2 * (ncol0 + TC) <= slen;
+      if (pre_ok) {
+#pragma unroll
+        for (int rr = 0; rr < RPT; ++rr) {
+          const uint32_t ch0 = tid * CPT + rr * JPR, v = ch0 / CPR;
+          if (!rhave[rr]) continue;
+#pragma unroll
+          for (int j = 0; j < JPR; ++j)
+            pre[rr * JPR + j] = *reinterpret_cast<const uint4 *>(
+                SH + uint64_t(v) * sstride + 2 * ncol0 + 16 * (ch0 % CPR + j));
         }
       }
     }
