@@ -8,7 +8,7 @@
  * Pinned against: (1) the reference's golden tables
  * (include/ec-cpp/table_f2e16.hpp, via tests/golden/tables.json digests) and
  * (2) outputs of the reference ec-cpp itself, compiled from
- * /root/reference by oracle/Makefile into oracle/_ref/ (tests/golden/*.json
+ * /root/reference by oracle/Makefile into oracle/_ref/ (the tests/golden JSON files
  * produced by tests/golden/make_golden.py).
  *
  * Every function names the reference file:line it restates.
