@@ -197,12 +197,26 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   const uint64_t ncols = slen / 2;
   const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);
   const uint64_t total = uint64_t(tiles_pp) * batch;
+  // per-row metadata of rows v = tid, tid + 512 of a tile's payload: bit 16 =
+  // present (and < nv), bits 0-15 = mul_index(E[v]).  Loaded one tile ahead so
+  // the gather's table loads and the output-table fill wait on one global
+  // latency instead of two (present/E, then the table).
+  auto load_meta = [&](uint64_t tl, uint32_t (&m)[2]) {
+    const uint64_t bb = tl / tiles_pp;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const uint32_t v = tid + half * THREADS;
+      const uint32_t p = present[bb * N + v], e = elog[bb * N + v];
+      m[half] = mul_index(e) | ((p != 0 && int(v) < nv) ? 0x10000u : 0u);
+    }
+  };
+  uint32_t meta[2] = {0, 0}, meta_next[2] = {0, 0};
+  if (blockIdx.x < total) load_meta(blockIdx.x, meta);
   for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
     const uint64_t b = tile / tiles_pp;
     const uint64_t col0 = (tile % tiles_pp) * COLS;
     const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
     const uint8_t *pr = present + b * N;
-    const uint16_t *E = elog + b * N;
     uint8_t *O = out + b * ostride;
 
     // ---- phase 1: gather + scale rows v = tid, tid + 512 (decode_main:174-177)
@@ -215,7 +229,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       uint32_t l[8], h[8];
 #pragma unroll
       for (int g = 0; g < 8; ++g) l[g] = h[g] = 0;
-      if (int(v) < nv && pr[v]) {
+      if (meta[half] & 0x10000u) {
         const uint8_t *row = SH + uint64_t(v) * sstride + 2 * col0;
         uint32_t w[16];
         const uint64_t avail = slen - 2 * col0;  // bytes of this row inside the tile
@@ -240,7 +254,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         }
         Tab T;
         if (DEC_ABL & 2) Tabs::load(tabs, v & 1023, T);
-        else load_tab(t.mtab, mul_index(E[v]), T);
+        else load_tab(t.mtab, meta[half] & 0xffffu, T);
 #pragma unroll
         for (int g = 0; g < 8; ++g) {  // columns 4g..4g+3: words (h0 l0 h1 l1)(h2 l2 h3 l3)
           const uint32_t a = w[2 * g], c = w[2 * g + 1];
@@ -252,6 +266,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       for (int g = 0; g < 8; ++g)
         *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l[g], h[g]);
     }
+    if (tile + gridDim.x < total) load_meta(tile + gridDim.x, meta_next);
     STAMP(2);
     __syncthreads();
     STAMP(3);
@@ -361,7 +376,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     STAMP(6);
     __syncthreads();  // every wave is done with its region: reuse them for E[y] tables
     if (!(DEC_ABL & 16))
-      OutTabs::fill(regions, t.mtab, K, [&](uint32_t y) { return mul_index(E[y]); }, tid, THREADS);
+      OutTabs::fill(regions, t.mtab, K, [&](uint32_t y) { return mul_index(elog[(tile / tiles_pp) * N + y]); }, tid, THREADS);
     STAMP(7);
     {
       // q bit0 = p6, bit1 = p7; lane bits = p0..p5.  Positions < 256 only.
@@ -500,6 +515,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       }
     }
     STAMP(10);
+    meta[0] = meta_next[0];
+    meta[1] = meta_next[1];
   }
 #ifdef DEC_STAMP
   if ((threadIdx.x & 63) == 0)
