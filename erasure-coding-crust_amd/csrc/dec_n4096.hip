@@ -113,6 +113,19 @@ reconstruct_n4096(
     const uint16_t *E = elog + b * N;
     uint8_t *O = out + b * ostride;
     S16 P, Qa;  // the two accumulators of the linearised cross-quarter stages
+    // gather-row metadata of a quarter (rows 1024q + tid, + 512): bit 16 = present
+    // (and < nv), bits 0-15 = mul_index(E[v]).  The next quarter's is loaded
+    // right after a quarter's gather, so its gather waits on one global latency
+    // (the table and the row) instead of two (present/E first).
+    uint32_t mq[1024 / THREADS];
+    const auto load_meta = [&](const int q, const uint32_t tq) __attribute__((always_inline)) {
+#pragma unroll
+      for (int half = 0; half < 1024 / THREADS; ++half) {
+        const uint32_t v = 1024 * q + tq + half * THREADS;
+        const uint32_t pv = pr[v], ev = E[v];
+        mq[half] = mul_index(ev) | ((pv != 0 && int(v) < nv) ? 0x10000u : 0u);
+      }
+    };
 
     // ---- IFFT quarters 3, 2, 1, 0 (quarter 0's tables stay for the FFT), each
     // folded into P and Qa as soon as it is transformed
@@ -135,7 +148,7 @@ reconstruct_n4096(
         uint32_t l[8], h[8];
 #pragma unroll
         for (int g = 0; g < 8; ++g) l[g] = h[g] = 0;
-        if (int(v) < nv && pr[v]) {
+        if (mq[half] & 0x10000u) {
           const uint8_t *row = SH + uint64_t(v) * sstride + 2 * col0;
           uint32_t w[16];
           const uint64_t avail = slen - 2 * col0;
@@ -152,7 +165,7 @@ reconstruct_n4096(
             load_row_tail64(row, avail, w);
           }
           Tab T;
-          load_tab(t.mtab, mul_index(E[v]), T);
+          load_tab(t.mtab, mq[half] & 0xffffu, T);
 #pragma unroll
           for (int g = 0; g < 8; ++g) {
             const uint32_t a = w[2 * g], c = w[2 * g + 1];
@@ -164,6 +177,7 @@ reconstruct_n4096(
         for (int g = 0; g < 8; ++g)
           *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(vl)) = make_uint2(l[g], h[g]);
       }
+      if (q > 0) load_meta(q - 1, tq);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // table image landed
       lds_barrier();
       __builtin_amdgcn_sched_barrier(0);
@@ -194,6 +208,7 @@ reconstruct_n4096(
     for (int r = 0; r < 16; ++r) P.l[r] = P.h[r] = Qa.l[r] = Qa.h[r] = 0;
     // a quarter wholly at or above n_validators holds no received symbol: its
     // IFFT is zero and adds nothing (n = 4096 with n_validators <= 3072)
+    load_meta(NQ == 4 && 3 * 1024 < nv ? 3 : NQ == 4 ? 2 : 1, tid);
     if constexpr (NQ == 4) {
       if (3 * 1024 < nv) quarter(3);
       quarter(2);
