@@ -70,6 +70,7 @@ bool encode_host(const CodeParams &p, const uint8_t *payload, size_t len, HostCt
       !ensure_dev(reinterpret_cast<void **>(&c->d_out), &c->d_out_cap, size_t(p.nv) * dstride))
     return false;
   ScratchLease lease(d, encode_scratch_bytes(p, len, 1), c->stream);
+  if (!lease.ok()) return false;
   void *scratch = lease.ptr();
   std::memcpy(c->h_in, payload, len);
   if (!hip_check(hipMemcpyAsync(c->d_in, c->h_in, len, hipMemcpyHostToDevice, c->stream), "H2D") ||
@@ -93,9 +94,7 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
   const size_t dstride = dev_pitch(sl);
   if (!ensure_dev(reinterpret_cast<void **>(&c->d_in), &c->d_in_cap, size_t(p.nv) * dstride) ||
       !ensure_dev(reinterpret_cast<void **>(&c->d_out), &c->d_out_cap, out_bytes) ||
-      !ensure_host(&c->h_out, &c->h_out_cap, out_bytes) ||
-      !ensure_dev(reinterpret_cast<void **>(&c->d_present), &c->d_present_cap, p.n) ||
-      !ensure_dev(reinterpret_cast<void **>(&c->d_elog), &c->d_elog_cap, size_t(p.n) * 2))
+      !ensure_host(&c->h_out, &c->h_out_cap, out_bytes))
     return false;
   bool all_systematic = true;
   for (uint32_t y = 0; y < p.k; ++y) all_systematic &= present[y] != 0;
@@ -110,19 +109,22 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
                    "systematic launch"))
       return false;
   } else {
-    const uint16_t *fold = device_fold(d, p.n);
-    if (!fold) return false;
+    // the pattern's locator: computed once per device, then reused (§8f row 3)
+    std::shared_ptr<const Locator> loc = cached_locator(d, p, present, c->stream);
+    if (!loc) return false;
     ScratchLease lease(d, reconstruct_scratch_bytes(p, sl, 1), c->stream);
+    if (!lease.ok()) return false;
     void *scratch = lease.ptr();
-    if (!hip_check(hipMemcpyAsync(c->d_present, present.data(), p.n, hipMemcpyHostToDevice,
-                                  c->stream),
-                   "H2D present") ||
-        !hip_check(launch_error_locator(p, c->d_present, 1, fold, c->d_elog, nullptr, c->stream),
-                   "error locator launch") ||
-        !hip_check(launch_reconstruct(p, device_tables(d), c->d_in, sl, dstride, c->d_present,
-                                      c->d_elog, 1, c->d_out, out_bytes, scratch, c->stream),
+    if (!hip_check(launch_reconstruct(p, device_tables(d), c->d_in, sl, dstride, loc->d_present,
+                                      loc->d_elog, nullptr, 1, c->d_out, out_bytes, scratch,
+                                      c->stream),
                    "reconstruct launch"))
       return false;
+    // `loc` is released only after the stream has finished with it
+    return hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost,
+                                    c->stream),
+                     "D2H") &&
+           hip_check(hipStreamSynchronize(c->stream), "reconstruct");
   }
   return hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost,
                                   c->stream),
@@ -362,6 +364,7 @@ NPRSResult ECCR_AMD_encode_batch(unsigned long nv, const uint8_t *d_payloads, un
   DeviceState *d = device_state();
   if (!d) return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
   ScratchLease lease(d, encode_scratch_bytes(p, plen, batch), static_cast<hipStream_t>(stream));
+  if (!lease.ok()) return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
   void *scratch = lease.ptr();
   if (!hip_check(launch_encode(p, device_tables(d), d_payloads, plen, pstride, batch, d_shards,
                                sstride, scratch, static_cast<hipStream_t>(stream)),
@@ -378,9 +381,77 @@ NPRSResult ECCR_AMD_error_locator(unsigned long nv, const uint8_t *d_present, un
   DeviceState *d = device_state();
   const uint16_t *fold = d ? device_fold(d, p.n) : nullptr;
   if (!fold) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-  if (!hip_check(launch_error_locator(p, d_present, batch, fold, d_err_log, nullptr,
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  if (batch <= 1) {
+    if (!hip_check(launch_error_locator(p, d_present, batch, fold, nullptr, d_err_log, s),
+                   "error locator launch"))
+      return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+    return result(NPRS_RESULT_OK);
+  }
+  // one locator per distinct pattern (§8f row 3), then copied to its followers
+  const size_t pat_bytes = (batch * 4 + 255) / 256 * 256;
+  ScratchLease lease(d, pat_bytes + dedup_scratch_bytes(batch), s);
+  if (!lease.ok()) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  uint32_t *pat = static_cast<uint32_t *>(lease.ptr());
+  void *work = static_cast<uint8_t *>(lease.ptr()) + pat_bytes;
+  if (!hip_check(launch_dedup_patterns(p, d_present, batch, pat, work, s), "pattern dedup") ||
+      !hip_check(launch_error_locator(p, d_present, batch, fold, pat, d_err_log, s),
+                 "error locator launch") ||
+      !hip_check(launch_broadcast_locators(p, pat, batch, d_err_log, s), "locator broadcast"))
+    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  return result(NPRS_RESULT_OK);
+}
+
+NPRSResult ECCR_AMD_dedup_patterns(unsigned long nv, const uint8_t *d_present, unsigned long batch,
+                                   uint32_t *d_pattern, void *stream) {
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag != NPRS_RESULT_OK) return r;
+  DeviceState *d = device_state();
+  if (!d) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  ScratchLease lease(d, dedup_scratch_bytes(batch), s);
+  if (!lease.ok() ||
+      !hip_check(launch_dedup_patterns(p, d_present, batch, d_pattern, lease.ptr(), s), "pattern dedup"))
+    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  return result(NPRS_RESULT_OK);
+}
+
+NPRSResult ECCR_AMD_error_locator_patterns(unsigned long nv, const uint8_t *d_present,
+                                           const uint32_t *d_pattern, unsigned long batch,
+                                           uint16_t *d_err_log, void *stream) {
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag != NPRS_RESULT_OK) return r;
+  DeviceState *d = device_state();
+  const uint16_t *fold = d ? device_fold(d, p.n) : nullptr;
+  if (!fold) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  if (!hip_check(launch_error_locator(p, d_present, batch, fold, d_pattern, d_err_log,
                                       static_cast<hipStream_t>(stream)),
                  "error locator launch"))
+    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  return result(NPRS_RESULT_OK);
+}
+
+NPRSResult ECCR_AMD_reconstruct_batch_patterns(unsigned long nv, const uint8_t *d_shards,
+                                               unsigned long slen, unsigned long sstride,
+                                               const uint8_t *d_present, const uint16_t *d_err_log,
+                                               const uint32_t *d_pattern, unsigned long batch,
+                                               uint8_t *d_out, unsigned long ostride, void *stream) {
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag != NPRS_RESULT_OK) return r;
+  if (slen % 2 != 0) return result(NPRS_RESULT_UNEVEN_LENGTH);
+  if (sstride < slen || ostride < slen * p.k) return result(NPRS_RESULT_NON_UNIFORM_CHUNKS);
+  DeviceState *d = device_state();
+  if (!d) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  ScratchLease lease(d, reconstruct_scratch_bytes(p, slen, batch), static_cast<hipStream_t>(stream));
+  if (!lease.ok()) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  void *scratch = lease.ptr();
+  if (!hip_check(launch_reconstruct(p, device_tables(d), d_shards, slen, sstride, d_present,
+                                    d_err_log, d_pattern, batch, d_out, ostride, scratch,
+                                    static_cast<hipStream_t>(stream)),
+                 "reconstruct launch"))
     return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
   return result(NPRS_RESULT_OK);
 }
@@ -390,20 +461,14 @@ NPRSResult ECCR_AMD_reconstruct_batch(unsigned long nv, const uint8_t *d_shards,
                                       const uint8_t *d_present, const uint16_t *d_err_log,
                                       unsigned long batch, uint8_t *d_out,
                                       unsigned long ostride, void *stream) {
-  CodeParams p;
-  NPRSResult r = params_or_error(nv, &p);
-  if (r.tag != NPRS_RESULT_OK) return r;
-  if (slen % 2 != 0) return result(NPRS_RESULT_UNEVEN_LENGTH);
-  if (sstride < slen || ostride < slen * p.k) return result(NPRS_RESULT_NON_UNIFORM_CHUNKS);
+  return ECCR_AMD_reconstruct_batch_patterns(nv, d_shards, slen, sstride, d_present, d_err_log,
+                                             nullptr, batch, d_out, ostride, stream);
+}
+
+NPRSResult ECCR_AMD_locator_cache_stats(unsigned long *hits, unsigned long *misses) {
   DeviceState *d = device_state();
   if (!d) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-  ScratchLease lease(d, reconstruct_scratch_bytes(p, slen, batch), static_cast<hipStream_t>(stream));
-  void *scratch = lease.ptr();
-  if (!hip_check(launch_reconstruct(p, device_tables(d), d_shards, slen, sstride, d_present,
-                                    d_err_log, batch, d_out, ostride, scratch,
-                                    static_cast<hipStream_t>(stream)),
-                 "reconstruct launch"))
-    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  locator_cache_stats(d, hits, misses);
   return result(NPRS_RESULT_OK);
 }
 

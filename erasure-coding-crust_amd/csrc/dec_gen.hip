@@ -80,6 +80,7 @@ template <int L, int KB>
 __global__ void __launch_bounds__(THREADS) reconstruct_gen(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
+    const uint32_t *__restrict__ pattern,
     uint8_t *__restrict__ out, uint64_t ostride, int nv, int k, uint32_t batch, DevTables t) {
   constexpr int N = 1 << L;
   constexpr uint32_t NM = N - 1;
@@ -122,8 +123,9 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
     const uint64_t b = tile / tiles_pp;
     const uint64_t col0 = (tile % tiles_pp) * TC;
     const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
-    const uint8_t *pr = present + b * N;
-    const uint16_t *E = elog + b * N;
+    const uint64_t pt = pattern ? pattern[b] : b;  // erasure pattern of payload b
+    const uint8_t *pr = present + pt * N;
+    const uint16_t *E = elog + pt * N;
     uint8_t *O = out + b * ostride;
 
     __syncthreads();  // previous tile's readers of the regions / output tables are done
@@ -304,22 +306,18 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
 template <int L, int KB>
 hipError_t launch_l(const CodeParams &p, const DevTables &t, const uint8_t *d_shards, size_t slen,
                     size_t sstride, const uint8_t *d_present, const uint16_t *d_err_log,
+                                    const uint32_t *d_pattern,
                     size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&reconstruct_gen<L, KB>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    if (e != hipSuccess) return e;
-  }
+  int cus = 0;
+  if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&reconstruct_gen<L, KB>),
+                                          LDS_BYTES, &cus);
+      e != hipSuccess)
+    return e;
   constexpr int TC = WAVES * 4 * (1024 >> L);
   const size_t tiles = (slen / 2 + TC - 1) / TC * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   hipLaunchKernelGGL((reconstruct_gen<L, KB>), dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
-                     uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out,
+                     uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, d_out,
                      uint64_t(ostride), int(p.nv), int(p.k), uint32_t(batch), t);
   return hipGetLastError();
 }
@@ -335,10 +333,11 @@ bool decgen_applicable(const CodeParams &p) {  // the (n, k) instantiated below
 hipError_t launch_reconstruct_gen(const CodeParams &p, const DevTables &t,
                                   const uint8_t *d_shards, size_t slen, size_t sstride,
                                   const uint8_t *d_present, const uint16_t *d_err_log,
+                                    const uint32_t *d_pattern,
                                   size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
 #define ECAMD_DG(Lv, KBv)                                                                   \
   if (p.n == (1u << Lv) && p.k == (1u << KBv))                                             \
-    return launch_l<Lv, KBv>(p, t, d_shards, slen, sstride, d_present, d_err_log, batch, d_out, \
+    return launch_l<Lv, KBv>(p, t, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch, d_out, \
                              ostride, s);
   // every (n, k) of 46 <= n_validators <= 765 (decgen_applicable)
   ECAMD_DG(6, 4)

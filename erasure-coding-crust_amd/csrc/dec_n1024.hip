@@ -181,6 +181,7 @@ __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ?
 __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
+    const uint32_t *__restrict__ pattern,
     uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t batch, DevTables t) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
@@ -202,11 +203,11 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   // the gather's table loads and the output-table fill wait on one global
   // latency instead of two (present/E, then the table).
   auto load_meta = [&](uint64_t tl, uint32_t (&m)[2]) {
-    const uint64_t bb = tl / tiles_pp;
+    const uint64_t bb = tl / tiles_pp, pt = pattern ? pattern[bb] : bb;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const uint32_t v = tid + half * THREADS;
-      const uint32_t p = present[bb * N + v], e = elog[bb * N + v];
+      const uint32_t p = present[pt * N + v], e = elog[pt * N + v];
       m[half] = mul_index(e) | ((p != 0 && int(v) < nv) ? 0x10000u : 0u);
     }
   };
@@ -215,8 +216,10 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
     const uint64_t b = tile / tiles_pp;
     const uint64_t col0 = (tile % tiles_pp) * COLS;
+    const uint64_t pt = pattern ? pattern[b] : b;  // erasure pattern of payload b
     const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
-    const uint8_t *pr = present + b * N;
+    const uint8_t *pr = present + pt * N;
+    const uint16_t *E = elog + pt * N;
     uint8_t *O = out + b * ostride;
 
     // ---- phase 1: gather + scale rows v = tid, tid + 512 (decode_main:174-177)
@@ -376,7 +379,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     STAMP(6);
     __syncthreads();  // every wave is done with its region: reuse them for E[y] tables
     if (!(DEC_ABL & 16))
-      OutTabs::fill(regions, t.mtab, K, [&](uint32_t y) { return mul_index(elog[(tile / tiles_pp) * N + y]); }, tid, THREADS);
+      OutTabs::fill(regions, t.mtab, K, [&](uint32_t y) { return mul_index(E[y]); }, tid, THREADS);
     STAMP(7);
     {
       // q bit0 = p6, bit1 = p7; lane bits = p0..p5.  Positions < 256 only.
@@ -529,21 +532,17 @@ bool n1024_applicable(const CodeParams &p) { return p.n == 1024 && p.k == 256; }
 hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
                                     const uint8_t *d_shards, size_t slen, size_t sstride,
                                     const uint8_t *d_present, const uint16_t *d_err_log,
+                                    const uint32_t *d_pattern,
                                     size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&reconstruct_n1024),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    if (e != hipSuccess) return e;
-  }
+  int cus = 0;
+  if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&reconstruct_n1024),
+                                          LDS_BYTES, &cus);
+      e != hipSuccess)
+    return e;
   const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   hipLaunchKernelGGL(reconstruct_n1024, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
-                     uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out,
+                     uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, d_out,
                      uint64_t(ostride), int(p.nv), uint32_t(batch), t);
   return hipGetLastError();
 }

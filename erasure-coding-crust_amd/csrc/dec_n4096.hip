@@ -90,6 +90,7 @@ __attribute__((amdgpu_waves_per_eu(1, 1)))
 reconstruct_n4096(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
+    const uint32_t *__restrict__ pattern,
     uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t K, uint32_t batch,
     DevTables t, Lin lin) {
   constexpr int N = 1024 * NQ;
@@ -109,8 +110,9 @@ reconstruct_n4096(
     const uint64_t b = tile / tiles_pp;
     const uint64_t col0 = (tile % tiles_pp) * COLS;
     const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
-    const uint8_t *pr = present + b * N;
-    const uint16_t *E = elog + b * N;
+    const uint64_t pt = pattern ? pattern[b] : b;  // erasure pattern of payload b
+    const uint8_t *pr = present + pt * N;
+    const uint16_t *E = elog + pt * N;
     uint8_t *O = out + b * ostride;
     S16 P, Qa;  // the two accumulators of the linearised cross-quarter stages
     // gather-row metadata of a quarter (rows 1024q + tid, + 512): bit 16 = present
@@ -342,30 +344,22 @@ bool n4096_applicable(const CodeParams &p) {  // the (n, k) instantiated below
 hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
                                     const uint8_t *d_shards, size_t slen, size_t sstride,
                                     const uint8_t *d_present, const uint16_t *d_err_log,
+                                    const uint32_t *d_pattern,
                                     size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-    const void *fns[] = {reinterpret_cast<const void *>(&reconstruct_n4096<4, 10>),
-                         reinterpret_cast<const void *>(&reconstruct_n4096<4, 9>),
-                         reinterpret_cast<const void *>(&reconstruct_n4096<2, 9>),
-                         reinterpret_cast<const void *>(&reconstruct_n4096<2, 8>)};
-    for (const void *f : fns) {
-      const hipError_t e =
-          hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-      if (e != hipSuccess) return e;
-    }
-  }
+  int cus = 0;
+  const void *fn = nullptr;
+  if (p.n == 4096) fn = p.k == 1024 ? reinterpret_cast<const void *>(&reconstruct_n4096<4, 10>)
+                                    : reinterpret_cast<const void *>(&reconstruct_n4096<4, 9>);
+  else fn = p.k == 512 ? reinterpret_cast<const void *>(&reconstruct_n4096<2, 9>)
+                       : reinterpret_cast<const void *>(&reconstruct_n4096<2, 8>);
+  if (const hipError_t e = prepare_kernel(fn, LDS_BYTES, &cus); e != hipSuccess) return e;
   const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   static const Lin lin4 = n4096_lin(4), lin2 = n4096_lin(2);
 #define ECAMD_D4(NQv, KBv)                                                                    \
   if (p.n == 1024u * NQv && p.k == (1u << KBv))                                                  \
     hipLaunchKernelGGL((reconstruct_n4096<NQv, KBv>), dim3(grid), dim3(THREADS), LDS_BYTES, s,   \
-                       d_shards, uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_out, \
+                       d_shards, uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, d_out, \
                        uint64_t(ostride), int(p.nv), uint32_t(p.k), uint32_t(batch), t,         \
                        NQv == 4 ? lin4 : lin2);
   ECAMD_D4(4, 10)

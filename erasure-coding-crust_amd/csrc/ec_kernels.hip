@@ -78,18 +78,20 @@ __global__ void __launch_bounds__(kBlock) encode_g(const uint8_t *__restrict__ p
                                                    uint64_t plen, uint64_t pstride,
                                                    uint8_t *__restrict__ shards, uint64_t slen,
                                                    uint64_t sstride, int nv, int logn, int logk,
-                                                   int logG, DevTables t, uint2 *scratch) {
+                                                   int logG, uint32_t batch, DevTables t,
+                                                   uint2 *scratch) {
   extern __shared__ __attribute__((aligned(16))) uint2 smem[];
   const int k = 1 << logk, n = 1 << logn, G = 1 << logG;
   const uint64_t npieces = slen / 2;
   const uint64_t piece0 = uint64_t(blockIdx.x) * 4 * G;
-  const uint8_t *P = payloads + uint64_t(blockIdx.y) * pstride;
-  uint8_t *SH = shards + uint64_t(blockIdx.y) * nv * sstride;
   uint2 *S = smem, *Cf = smem + size_t(k) * G;
-  if (scratch) {
+  if (scratch) {  // one buffer per block, reused by its payloads in turn
     S = scratch + (uint64_t(blockIdx.y) * gridDim.x + blockIdx.x) * 2 * uint64_t(k) * G;
     Cf = S + size_t(k) * G;
   }
+  for (uint32_t b = blockIdx.y; b < batch; b += gridDim.y) {  // batch may exceed gridDim.y's limit
+  const uint8_t *P = payloads + uint64_t(b) * pstride;
+  uint8_t *SH = shards + uint64_t(b) * nv * sstride;
   // BE-unpack 4 pieces per group, zero-padded (poly_encoder.hpp:53-76); the
   // systematic shards are the data symbols themselves (poly_encoder.hpp:239)
   for (int e = threadIdx.x; e < k * G; e += blockDim.x) {
@@ -135,6 +137,7 @@ __global__ void __launch_bounds__(kBlock) encode_g(const uint8_t *__restrict__ p
     }
     __syncthreads();
   }
+  }
 }
 
 // poly_encoder.hpp:90-116 in the folded n-point form: one
@@ -143,10 +146,12 @@ __global__ void __launch_bounds__(kBlock) encode_g(const uint8_t *__restrict__ p
 __global__ void __launch_bounds__(kBlock) error_locator_g(const uint8_t *__restrict__ present,
                                                           int nv, int logn,
                                                           const uint16_t *__restrict__ fold,
+                                                          const uint32_t *__restrict__ pattern,
                                                           uint16_t *__restrict__ elog,
                                                           uint16_t *scratch) {
   extern __shared__ __attribute__((aligned(16))) uint16_t w16[];
   const int n = 1 << logn;
+  if (pattern && pattern[blockIdx.x] != blockIdx.x) return;  // computed by its pattern's leader
   const uint8_t *pr = present + uint64_t(blockIdx.x) * n;
   uint16_t *W = scratch ? scratch + uint64_t(blockIdx.x) * n : w16;
   for (int i = threadIdx.x; i < n; i += blockDim.x) W[i] = (i < nv && pr[i]) ? 0 : 1;
@@ -175,6 +180,91 @@ __global__ void __launch_bounds__(kBlock) error_locator_g(const uint8_t *__restr
   }
 }
 
+// ---- erasure-pattern dedup: payloads whose erasure
+// patterns are equal share one locator.  The locator depends only on the
+// flags (present[i] != 0) of positions i < nv, and so do the hash and the
+// equality test below.
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// block per row: H = sum over present positions i of mix64(i) (order-free, so
+// a block-wide sum); never 0 (0 marks an empty hash slot)
+__global__ void __launch_bounds__(kBlock) pattern_hash(const uint8_t *__restrict__ present, int nv,
+                                                       int n, uint64_t *__restrict__ hash) {
+  __shared__ uint64_t part[kBlock / 64];
+  const uint8_t *pr = present + uint64_t(blockIdx.x) * n;
+  uint64_t h = 0;
+  for (int i = threadIdx.x; i < nv; i += kBlock)
+    if (pr[i]) h += mix64(uint64_t(i));
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < kBlock / 64; ++w) t += part[w];
+    hash[blockIdx.x] = t ? t : 1;
+  }
+}
+
+// thread per row: open-addressing insert, each slot keeps the smallest row
+// index with its hash
+__global__ void __launch_bounds__(kBlock) pattern_insert(const uint64_t *__restrict__ hash,
+                                                         uint32_t batch, unsigned long long *keys,
+                                                         uint32_t *vals, uint32_t cap) {
+  const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+  if (b >= batch) return;
+  const uint64_t h = hash[b];
+  for (uint32_t slot = uint32_t(h % cap), probe = 0; probe < cap; ++probe, slot = (slot + 1) % cap) {
+    const unsigned long long prev = atomicCAS(&keys[slot], 0ull, (unsigned long long)h);
+    if (prev == 0ull || prev == h) {
+      atomicMin(&vals[slot], b);
+      return;
+    }
+  }
+}
+
+// block per row: pattern[b] = the leader (smallest index) of b's hash if its
+// flags are identical to b's, else b itself (a hash collision: b keeps its own)
+__global__ void __launch_bounds__(kBlock) pattern_resolve(const uint8_t *__restrict__ present, int nv,
+                                                          int n, const uint64_t *__restrict__ hash,
+                                                          const unsigned long long *__restrict__ keys,
+                                                          const uint32_t *__restrict__ vals,
+                                                          uint32_t cap, uint32_t *__restrict__ pattern) {
+  __shared__ uint32_t leader;
+  __shared__ int differ;
+  const uint32_t b = blockIdx.x;
+  if (threadIdx.x == 0) {
+    const uint64_t h = hash[b];
+    uint32_t slot = uint32_t(h % cap);
+    for (uint32_t probe = 0; probe < cap && keys[slot] != h; ++probe) slot = (slot + 1) % cap;
+    leader = keys[slot] == h ? vals[slot] : b;
+    differ = 0;
+  }
+  __syncthreads();
+  const uint32_t l = leader;
+  if (l != b) {
+    const uint8_t *pb = present + uint64_t(b) * n, *pl = present + uint64_t(l) * n;
+    for (int i = threadIdx.x; i < nv; i += kBlock)
+      if ((pb[i] != 0) != (pl[i] != 0)) differ = 1;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) pattern[b] = (l != b && !differ) ? l : b;
+}
+
+// block per row: a follower's locator row = its leader's
+__global__ void __launch_bounds__(kBlock) pattern_broadcast(const uint32_t *__restrict__ pattern, int n,
+                                                            uint16_t *__restrict__ elog) {
+  const uint32_t b = blockIdx.x, l = pattern[b];
+  if (l == b) return;
+  const uint16_t *src = elog + uint64_t(l) * n;
+  uint16_t *dst = elog + uint64_t(b) * n;
+  for (int i = threadIdx.x; i < n; i += kBlock) dst[i] = src[i];
+}
+
 __device__ __forceinline__ uint32_t mul_index(uint32_t log_c) {  // 65535 == 0 (mod 65535)
   return log_c == 65535u ? 0u : log_c;
 }
@@ -184,20 +274,23 @@ __global__ void __launch_bounds__(kBlock) reconstruct_g(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
     uint8_t *__restrict__ out, uint64_t ostride, int nv, int logn, int logk, int logG,
-    DevTables t, uint2 *scratch) {
+    uint32_t batch, const uint32_t *__restrict__ pattern, DevTables t, uint2 *scratch) {
   extern __shared__ __attribute__((aligned(16))) uint2 smem[];
   const int n = 1 << logn, k = 1 << logk, G = 1 << logG;
   const uint64_t npos = slen / 2;
   const uint64_t pos0 = uint64_t(blockIdx.x) * 4 * G;
-  const uint8_t *SH = shards + uint64_t(blockIdx.y) * nv * sstride;
-  const uint8_t *pr = present + uint64_t(blockIdx.y) * n;
-  const uint16_t *E = elog + uint64_t(blockIdx.y) * n;
-  uint8_t *O = out + uint64_t(blockIdx.y) * ostride;
   uint2 *S = smem, *D = smem + size_t(n) * G;
-  if (scratch) {
+  if (scratch) {  // one buffer per block, reused by its payloads in turn
     S = scratch + (uint64_t(blockIdx.y) * gridDim.x + blockIdx.x) * 2 * uint64_t(n) * G;
     D = S + size_t(n) * G;
   }
+  for (uint32_t b = blockIdx.y; b < batch; b += gridDim.y) {  // batch may exceed gridDim.y's limit
+  const uint64_t pt = pattern ? pattern[b] : b;  // erasure pattern of payload b
+  const uint8_t *SH = shards + uint64_t(b) * nv * sstride;
+  const uint8_t *pr = present + pt * n;
+  const uint16_t *E = elog + pt * n;
+  uint8_t *O = out + uint64_t(b) * ostride;
+  __syncthreads();  // the previous payload's readers of S / D are done
   // gather the column, multiply present symbols by the locator (decode_main:174-177)
   for (int e = threadIdx.x; e < n * G; e += blockDim.x) {
     const int g = e & (G - 1), v = e >> logG;
@@ -264,28 +357,34 @@ __global__ void __launch_bounds__(kBlock) reconstruct_g(
       }
     }
   }
+  }
 }
 
 // reed-solomon.hpp:143-179: out[2(i*k + y) ..] = shard_y[2i ..]
 __global__ void __launch_bounds__(kBlock) systematic_g(const uint8_t *__restrict__ shards,
                                                        uint64_t slen, uint64_t sstride, int nv,
                                                        int logk, uint8_t *__restrict__ out,
-                                                       uint64_t ostride) {
+                                                       uint64_t ostride, uint32_t batch) {
   const int k = 1 << logk;
   const uint64_t npos = slen / 2;
-  const uint8_t *SH = shards + uint64_t(blockIdx.y) * nv * sstride;
-  uint8_t *O = out + uint64_t(blockIdx.y) * ostride;
   const uint64_t total = npos * k;
-  for (uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < total;
-       e += uint64_t(gridDim.x) * blockDim.x) {
-    const uint64_t i = e >> logk;
-    const int y = int(e & (k - 1));
-    O[2 * e] = SH[uint64_t(y) * sstride + 2 * i];
-    O[2 * e + 1] = SH[uint64_t(y) * sstride + 2 * i + 1];
+  for (uint32_t b = blockIdx.y; b < batch; b += gridDim.y) {
+    const uint8_t *SH = shards + uint64_t(b) * nv * sstride;
+    uint8_t *O = out + uint64_t(b) * ostride;
+    for (uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < total;
+         e += uint64_t(gridDim.x) * blockDim.x) {
+      const uint64_t i = e >> logk;
+      const int y = int(e & (k - 1));
+      O[2 * e] = SH[uint64_t(y) * sstride + 2 * i];
+      O[2 * e + 1] = SH[uint64_t(y) * sstride + 2 * i + 1];
+    }
   }
 }
 
 int ilog2(uint32_t v) { return 31 - __builtin_clz(v); }
+
+// payload slots in gridDim.y (hardware limit 65535); the kernels loop over the rest
+size_t grid_y(size_t batch) { return batch < 65535 ? batch : 65535; }
 
 int groups_for(uint32_t size) {  // byte-planar groups per workgroup
   if (size >= kLdsSlots) return 1;
@@ -300,7 +399,7 @@ size_t encode_scratch_bytes(const CodeParams &p, size_t plen, size_t batch) {
   if (p.k <= uint32_t(kLdsSlots)) return 0;
   const size_t pieces = shard_len(p.k, plen) / 2;
   const size_t tiles = (pieces + 3) / 4;
-  return tiles * batch * 2 * size_t(p.k) * sizeof(uint2);
+  return tiles * grid_y(batch) * 2 * size_t(p.k) * sizeof(uint2);
 }
 
 hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
@@ -321,67 +420,102 @@ hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t 
   const size_t tiles = (sl / 2 + 4 * G - 1) / (4 * G);
   const bool lds = p.k <= uint32_t(kLdsSlots);
   const size_t shm = lds ? 2 * size_t(p.k) * G * sizeof(uint2) : 0;
-  dim3 grid((unsigned)tiles, (unsigned)batch);
+  dim3 grid((unsigned)tiles, (unsigned)grid_y(batch));
   hipLaunchKernelGGL(encode_g, grid, dim3(kBlock), shm, s, d_payloads, uint64_t(plen),
                      uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride), int(p.nv),
-                     ilog2(p.n), ilog2(p.k), ilog2(uint32_t(G)), t,
+                     ilog2(p.n), ilog2(p.k), ilog2(uint32_t(G)), uint32_t(batch), t,
                      lds ? nullptr : static_cast<uint2 *>(scratch));
   return hipGetLastError();
 }
 
-size_t error_locator_scratch_bytes(const CodeParams &p, size_t batch) {
-  return p.n > 65536u ? batch * p.n * 2 : 0;
+namespace {
+uint32_t dedup_cap(size_t batch) {  // hash slots: a power of two >= 2 * batch
+  uint32_t c = 64;
+  while (c < 2 * batch) c <<= 1;
+  return c;
+}
+}  // namespace
+
+size_t dedup_scratch_bytes(size_t batch) {
+  const size_t cap = dedup_cap(batch);
+  return batch * 8 + cap * 8 + cap * 4;  // hashes, keys, values
+}
+
+hipError_t launch_dedup_patterns(const CodeParams &p, const uint8_t *d_present, size_t batch,
+                                 uint32_t *d_pattern, void *scratch, hipStream_t s) {
+  if (batch == 0) return hipSuccess;
+  if (!scratch) return hipErrorInvalidValue;
+  const uint32_t cap = dedup_cap(batch);
+  uint64_t *hash = static_cast<uint64_t *>(scratch);
+  unsigned long long *keys = reinterpret_cast<unsigned long long *>(hash + batch);
+  uint32_t *vals = reinterpret_cast<uint32_t *>(keys + cap);
+  if (const hipError_t e = hipMemsetAsync(keys, 0, size_t(cap) * 8, s); e != hipSuccess) return e;
+  if (const hipError_t e = hipMemsetAsync(vals, 0xff, size_t(cap) * 4, s); e != hipSuccess) return e;
+  hipLaunchKernelGGL(pattern_hash, dim3(unsigned(batch)), dim3(kBlock), 0, s, d_present, int(p.nv),
+                     int(p.n), hash);
+  hipLaunchKernelGGL(pattern_insert, dim3(unsigned((batch + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                     hash, uint32_t(batch), keys, vals, cap);
+  hipLaunchKernelGGL(pattern_resolve, dim3(unsigned(batch)), dim3(kBlock), 0, s, d_present,
+                     int(p.nv), int(p.n), hash, keys, vals, cap, d_pattern);
+  return hipGetLastError();
 }
 
 hipError_t launch_error_locator(const CodeParams &p, const uint8_t *d_present, size_t batch,
-                                const uint16_t *d_fold, uint16_t *d_err_log, void *scratch,
-                                hipStream_t s) {
+                                const uint16_t *d_fold, const uint32_t *d_pattern,
+                                uint16_t *d_err_log, hipStream_t s) {
   if (batch == 0) return hipSuccess;
   const size_t shm = size_t(p.n) * sizeof(uint16_t);
-  if (shm > 65536) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&error_locator_g),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, int(shm));
-    if (e != hipSuccess) return e;
-  }
+  int cus = 0;
+  if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&error_locator_g), 65536 * 2, &cus);
+      e != hipSuccess)
+    return e;
   hipLaunchKernelGGL(error_locator_g, dim3(unsigned(batch)), dim3(kBlock), shm, s, d_present,
-                     int(p.nv), ilog2(p.n), d_fold, d_err_log, static_cast<uint16_t *>(nullptr));
-  (void)scratch;
+                     int(p.nv), ilog2(p.n), d_fold, d_pattern, d_err_log,
+                     static_cast<uint16_t *>(nullptr));
+  return hipGetLastError();
+}
+
+hipError_t launch_broadcast_locators(const CodeParams &p, const uint32_t *d_pattern, size_t batch,
+                                     uint16_t *d_err_log, hipStream_t s) {
+  if (batch == 0) return hipSuccess;
+  hipLaunchKernelGGL(pattern_broadcast, dim3(unsigned(batch)), dim3(kBlock), 0, s, d_pattern,
+                     int(p.n), d_err_log);
   return hipGetLastError();
 }
 
 size_t reconstruct_scratch_bytes(const CodeParams &p, size_t slen, size_t batch) {
   if (p.n <= uint32_t(kLdsSlots)) return 0;
   const size_t tiles = (slen / 2 + 3) / 4;
-  return tiles * batch * 2 * size_t(p.n) * sizeof(uint2);
+  return tiles * grid_y(batch) * 2 * size_t(p.n) * sizeof(uint2);
 }
 
 hipError_t launch_reconstruct(const CodeParams &p, const DevTables &t, const uint8_t *d_shards,
                               size_t slen, size_t sstride, const uint8_t *d_present,
-                              const uint16_t *d_err_log, size_t batch, uint8_t *d_out,
-                              size_t ostride, void *scratch, hipStream_t s) {
+                              const uint16_t *d_err_log, const uint32_t *d_pattern, size_t batch,
+                              uint8_t *d_out, size_t ostride, void *scratch, hipStream_t s) {
   if (batch == 0 || slen < 2) return hipSuccess;
   const bool aligned = (reinterpret_cast<uintptr_t>(d_shards) % 16 == 0) &&
                        (reinterpret_cast<uintptr_t>(d_out) % 8 == 0) && sstride % 16 == 0 &&
                        (batch == 1 || ostride % 8 == 0);
   if (aligned && n1024_applicable(p))
-    return launch_reconstruct_n1024(p, t, d_shards, slen, sstride, d_present, d_err_log, batch,
+    return launch_reconstruct_n1024(p, t, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch,
                                     d_out, ostride, s);
   if (aligned && n4096_applicable(p) && reinterpret_cast<uintptr_t>(d_out) % 16 == 0 &&
       (batch == 1 || ostride % 16 == 0))
-    return launch_reconstruct_n4096(p, t, d_shards, slen, sstride, d_present, d_err_log, batch,
+    return launch_reconstruct_n4096(p, t, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch,
                                     d_out, ostride, s);
   if (aligned && decgen_applicable(p) && reinterpret_cast<uintptr_t>(d_out) % 16 == 0 &&
       (batch == 1 || ostride % 16 == 0))
-    return launch_reconstruct_gen(p, t, d_shards, slen, sstride, d_present, d_err_log, batch,
+    return launch_reconstruct_gen(p, t, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch,
                                   d_out, ostride, s);
   const int G = groups_for(p.n);
   const size_t tiles = (slen / 2 + 4 * G - 1) / (4 * G);
   const bool lds = p.n <= uint32_t(kLdsSlots);
   const size_t shm = lds ? 2 * size_t(p.n) * G * sizeof(uint2) : 0;
-  dim3 grid((unsigned)tiles, (unsigned)batch);
+  dim3 grid((unsigned)tiles, (unsigned)grid_y(batch));
   hipLaunchKernelGGL(reconstruct_g, grid, dim3(kBlock), shm, s, d_shards, uint64_t(slen),
                      uint64_t(sstride), d_present, d_err_log, d_out, uint64_t(ostride), int(p.nv),
-                     ilog2(p.n), ilog2(p.k), ilog2(uint32_t(G)), t,
+                     ilog2(p.n), ilog2(p.k), ilog2(uint32_t(G)), uint32_t(batch), d_pattern, t,
                      lds ? nullptr : static_cast<uint2 *>(scratch));
   return hipGetLastError();
 }
@@ -393,9 +527,9 @@ hipError_t launch_systematic(const CodeParams &p, const uint8_t *d_shards, size_
   const size_t total = slen / 2 * p.k;
   size_t blocks = (total + kBlock - 1) / kBlock;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(systematic_g, dim3(unsigned(blocks), unsigned(batch)), dim3(kBlock), 0, s,
-                     d_shards, uint64_t(slen), uint64_t(sstride), int(p.nv), ilog2(p.k), d_out,
-                     uint64_t(ostride));
+  hipLaunchKernelGGL(systematic_g, dim3(unsigned(blocks), unsigned(grid_y(batch))), dim3(kBlock), 0,
+                     s, d_shards, uint64_t(slen), uint64_t(sstride), int(p.nv), ilog2(p.k), d_out,
+                     uint64_t(ostride), uint32_t(batch));
   return hipGetLastError();
 }
 

@@ -23,6 +23,13 @@ struct DevTables {
   const uint8_t *timg = nullptr;    // kTabImages x kTabImageBytes
 };
 
+// Per (device, kernel), once and thread-safe: raise `fn`'s dynamic-LDS limit
+// to `lds_bytes` (if above the 64 KB default) and return the current device's
+// CU count in *cus.  The count is handed out only after the attribute call
+// succeeded, so no thread launches a kernel whose limit is not set yet; a
+// failed call is retried on the next launch (ec_runtime.cpp).
+hipError_t prepare_kernel(const void *fn, int lds_bytes, int *cus);
+
 // Scratch (global memory) needed by each launch for FFT sizes whose working
 // set does not fit LDS; 0 for the common sizes.
 size_t encode_scratch_bytes(const CodeParams &p, size_t payload_len, size_t batch);
@@ -32,15 +39,27 @@ hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t 
                          size_t payload_len, size_t payload_stride, size_t batch, uint8_t *d_shards,
                          size_t shard_stride, void *scratch, hipStream_t s);
 
+// Erasure locators (poly_encoder.hpp:90-116, folded form), one workgroup per
+// row of d_present.  d_pattern (nullable): rows b with d_pattern[b] != b are
+// skipped (their pattern's leader row holds the locator).
 hipError_t launch_error_locator(const CodeParams &p, const uint8_t *d_present, size_t batch,
-                                const uint16_t *d_fold, uint16_t *d_err_log, void *scratch,
-                                hipStream_t s);
-size_t error_locator_scratch_bytes(const CodeParams &p, size_t batch);
+                                const uint16_t *d_fold, const uint32_t *d_pattern,
+                                uint16_t *d_err_log, hipStream_t s);
+// Pattern dedup: d_pattern[b] = the smallest index whose
+// erasure pattern equals payload b's.  Needs dedup_scratch_bytes(batch).
+size_t dedup_scratch_bytes(size_t batch);
+hipError_t launch_dedup_patterns(const CodeParams &p, const uint8_t *d_present, size_t batch,
+                                 uint32_t *d_pattern, void *scratch, hipStream_t s);
+// follower rows of d_err_log <- their leader's row
+hipError_t launch_broadcast_locators(const CodeParams &p, const uint32_t *d_pattern, size_t batch,
+                                     uint16_t *d_err_log, hipStream_t s);
 
+// d_pattern (nullable): payload b's erasure pattern is row d_pattern[b] of
+// d_present / d_err_log (NULL: row b)
 hipError_t launch_reconstruct(const CodeParams &p, const DevTables &t, const uint8_t *d_shards,
                               size_t shard_len, size_t shard_stride, const uint8_t *d_present,
-                              const uint16_t *d_err_log, size_t batch, uint8_t *d_out,
-                              size_t out_stride, void *scratch, hipStream_t s);
+                              const uint16_t *d_err_log, const uint32_t *d_pattern, size_t batch,
+                              uint8_t *d_out, size_t out_stride, void *scratch, hipStream_t s);
 
 hipError_t launch_systematic(const CodeParams &p, const uint8_t *d_shards, size_t shard_len,
                              size_t shard_stride, size_t batch, uint8_t *d_out, size_t out_stride,
@@ -71,20 +90,20 @@ bool n1024_applicable(const CodeParams &p);
 hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
                                     const uint8_t *d_shards, size_t slen, size_t sstride,
                                     const uint8_t *d_present, const uint16_t *d_err_log,
-                                    size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s);
+                                    const uint32_t *d_pattern, size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s);
 
 // specialised kernels (dec_n4096.hip)
 bool n4096_applicable(const CodeParams &p);
 hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
                                     const uint8_t *d_shards, size_t slen, size_t sstride,
                                     const uint8_t *d_present, const uint16_t *d_err_log,
-                                    size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s);
+                                    const uint32_t *d_pattern, size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s);
 
 // register-blocked reconstruct for 64 <= n <= 1024, 16 <= k <= 512 (dec_gen.hip)
 bool decgen_applicable(const CodeParams &p);
 hipError_t launch_reconstruct_gen(const CodeParams &p, const DevTables &t,
                                   const uint8_t *d_shards, size_t slen, size_t sstride,
                                   const uint8_t *d_present, const uint16_t *d_err_log,
-                                  size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s);
+                                  const uint32_t *d_pattern, size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s);
 
 }  // namespace ecamd

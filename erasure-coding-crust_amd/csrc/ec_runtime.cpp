@@ -3,9 +3,11 @@
 
 #include <cstdio>
 #include <cstring>
+#include <list>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 namespace ecamd {
@@ -22,6 +24,9 @@ struct DeviceState {
   size_t scratch_cap = 0;
   hipEvent_t scratch_done = nullptr;  // the last lease's work on its stream
   bool scratch_used = false;
+  std::mutex loc_mu;
+  std::list<std::shared_ptr<const Locator>> loc;  // most recent first
+  unsigned long loc_hits = 0, loc_misses = 0;
 };
 
 namespace {
@@ -104,8 +109,32 @@ const uint16_t *device_fold(DeviceState *d, uint32_t n) {
   return p;
 }
 
+hipError_t prepare_kernel(const void *fn, int lds_bytes, int *cus) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void *>, bool> prepared;
+  static std::map<int, int> cu_count;
+  int dev = 0;
+  if (const hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(mu);
+  auto c = cu_count.find(dev);
+  if (c == cu_count.end()) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    c = cu_count.emplace(dev, n).first;
+  }
+  bool &done = prepared[{dev, fn}];
+  if (!done && lds_bytes > 65536) {
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    if (e != hipSuccess) return e;
+  }
+  done = true;
+  *cus = c->second;
+  return hipSuccess;
+}
+
 ScratchLease::ScratchLease(DeviceState *d, size_t bytes, hipStream_t stream)
-    : d_(d), s_(stream) {
+    : d_(d), s_(stream), want_(bytes) {
   if (!d || bytes == 0) return;
   d->scratch_mu.lock();
   held_ = true;
@@ -129,6 +158,56 @@ ScratchLease::~ScratchLease() {
   if (!d_->scratch_done) (void)hipEventCreateWithFlags(&d_->scratch_done, hipEventDisableTiming);
   d_->scratch_used = d_->scratch_done && hipEventRecord(d_->scratch_done, s_) == hipSuccess;
   d_->scratch_mu.unlock();
+}
+
+Locator::~Locator() {
+  if (ready) {
+    (void)hipEventSynchronize(ready);  // no copy / kernel still uses the buffers
+    (void)hipEventDestroy(ready);
+  }
+  if (d_present) (void)hipFree(d_present);
+  if (d_elog) (void)hipFree(d_elog);
+}
+
+std::shared_ptr<const Locator> cached_locator(DeviceState *d, const CodeParams &p,
+                                              const std::vector<uint8_t> &present,
+                                              hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(d->loc_mu);
+  for (auto it = d->loc.begin(); it != d->loc.end(); ++it)
+    if ((*it)->nv == p.nv && (*it)->present == present) {
+      std::shared_ptr<const Locator> hit = *it;
+      d->loc.erase(it);
+      d->loc.push_front(hit);
+      ++d->loc_hits;
+      if (!hip_ok(hipStreamWaitEvent(stream, hit->ready, 0), "locator wait")) return nullptr;
+      return hit;
+    }
+  ++d->loc_misses;
+  const uint16_t *fold = device_fold(d, p.n);
+  if (!fold) return nullptr;
+  auto L = std::make_shared<Locator>();
+  L->nv = p.nv;
+  L->present = present;
+  if (!hip_ok(hipMalloc(&L->d_present, p.n), "hipMalloc(locator)") ||
+      !hip_ok(hipMalloc(&L->d_elog, size_t(p.n) * 2), "hipMalloc(locator)") ||
+      !hip_ok(hipEventCreateWithFlags(&L->ready, hipEventDisableTiming), "hipEventCreate") ||
+      !hip_ok(hipMemcpyAsync(L->d_present, L->present.data(), p.n, hipMemcpyHostToDevice, stream),
+              "H2D present") ||
+      !hip_ok(launch_error_locator(p, L->d_present, 1, fold, nullptr, L->d_elog, stream),
+              "error locator launch") ||
+      !hip_ok(hipEventRecord(L->ready, stream), "hipEventRecord")) {
+    (void)hipStreamSynchronize(stream);  // nothing issued above may outlive L
+    return nullptr;
+  }
+  d->loc.push_front(L);
+  if (d->loc.size() > kLocatorCache) d->loc.pop_back();  // freed once its last user is done
+  return L;
+}
+
+void locator_cache_stats(DeviceState *d, unsigned long *hits, unsigned long *misses) {
+  std::lock_guard<std::mutex> lk(d->loc_mu);
+  if (hits) *hits = d->loc_hits;
+  if (misses) *misses = d->loc_misses;
 }
 
 bool ensure_host(uint8_t **p, size_t *cap, size_t need) {
@@ -155,7 +234,27 @@ bool ensure_dev(void **p, size_t *cap, size_t need) {
   return true;
 }
 
+HostCtx::~HostCtx() {
+  // the thread's work is finished (every C-ABI call synchronises its stream);
+  // release on the context's own device
+  int cur = -1;
+  const bool switched = hipGetDevice(&cur) == hipSuccess && cur != device && device >= 0 &&
+                        hipSetDevice(device) == hipSuccess;
+  if (stream) {
+    (void)hipStreamSynchronize(stream);
+    (void)hipStreamDestroy(stream);
+  }
+  for (uint8_t *h : {h_in, h_out})
+    if (h) (void)hipHostFree(h);
+  for (void *p : {static_cast<void *>(d_in), static_cast<void *>(d_out),
+                  static_cast<void *>(d_present), static_cast<void *>(d_elog)})
+    if (p) (void)hipFree(p);
+  if (switched) (void)hipSetDevice(cur);
+}
+
 HostCtx *host_ctx() {
+  // destroyed (buffers and stream released) at thread exit or when the
+  // thread switches devices
   thread_local std::unique_ptr<HostCtx> ctx;
   DeviceState *d = device_state();
   if (!d) return nullptr;

@@ -5,7 +5,9 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <vector>
 
 #include "ec_kernels.hpp"
 #include "gf_field.hpp"
@@ -31,17 +33,45 @@ class ScratchLease {
   ScratchLease(const ScratchLease &) = delete;
   ScratchLease &operator=(const ScratchLease &) = delete;
   void *ptr() const { return p_; }
+  // false if scratch was needed and could not be allocated (the caller must
+  // not launch: the kernels would run on a null buffer)
+  bool ok() const { return want_ == 0 || p_ != nullptr; }
 
  private:
   DeviceState *d_ = nullptr;
   hipStream_t s_ = nullptr;
+  size_t want_ = 0;
   void *p_ = nullptr;
   bool held_ = false;
 };
 
+// Per-pattern erasure-locator cache of the per-call C ABI (SURVEY.md §8f
+// row 3): the locator of a pattern (n_validators + present bitmap) is computed
+// once per device and reused while it is among the most recent kLocatorCache
+// patterns (the common case: the same validators missing for every block).
+constexpr size_t kLocatorCache = 64;
+struct Locator {
+  uint32_t nv = 0;
+  std::vector<uint8_t> present;  // the key: [n] flags
+  uint8_t *d_present = nullptr;  // [n] on the device
+  uint16_t *d_elog = nullptr;    // [n] log-domain multipliers (ECCR_AMD_error_locator)
+  hipEvent_t ready = nullptr;    // recorded after the locator kernel
+  ~Locator();                    // waits for `ready`, then frees
+};
+// The pattern's locator, computed on `stream` on a miss; on a hit `stream`
+// is ordered after the kernel that computed it.  nullptr on a HIP error.
+std::shared_ptr<const Locator> cached_locator(DeviceState *d, const CodeParams &p,
+                                              const std::vector<uint8_t> &present,
+                                              hipStream_t stream);
+void locator_cache_stats(DeviceState *d, unsigned long *hits, unsigned long *misses);
+
 // Growable buffers of one host thread (reentrancy = the reference's
 // thread_local scratch, reed-solomon.hpp:198-201).
 struct HostCtx {
+  HostCtx() = default;
+  HostCtx(const HostCtx &) = delete;
+  HostCtx &operator=(const HostCtx &) = delete;
+  ~HostCtx();  // synchronises and releases the stream and every buffer
   hipStream_t stream = nullptr;
   uint8_t *h_in = nullptr, *h_out = nullptr;  // pinned
   size_t h_in_cap = 0, h_out_cap = 0;

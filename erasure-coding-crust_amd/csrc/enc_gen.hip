@@ -290,16 +290,10 @@ template <int M>
 hipError_t launch_m(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                     size_t plen, size_t pstride, size_t batch, uint8_t *d_shards, size_t sstride,
                     hipStream_t s) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&encode_gen<M>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    if (e != hipSuccess) return e;
-  }
+  int cus = 0;
+  if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&encode_gen<M>), LDS_BYTES, &cus);
+      e != hipSuccess)
+    return e;
   const size_t sl = shard_len(p.k, plen);
   const size_t tiles = (sl / 2 + Geo<M>::TP - 1) / Geo<M>::TP * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));

@@ -203,18 +203,10 @@ size_t k1024_scratch_bytes(size_t plen, size_t batch) {
 hipError_t launch_encode_k1024(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                                size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                                size_t sstride, void *scratch, hipStream_t s) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-    for (const void *f : {reinterpret_cast<const void *>(&encode_k1024<0>),
-                          reinterpret_cast<const void *>(&encode_k1024<1>)}) {
-      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-      if (e != hipSuccess) return e;
-    }
-  }
+  int cus = 0;
+  for (const void *f : {reinterpret_cast<const void *>(&encode_k1024<0>),
+                        reinterpret_cast<const void *>(&encode_k1024<1>)})
+    if (const hipError_t e = prepare_kernel(f, LDS_BYTES, &cus); e != hipSuccess) return e;
   if (!scratch) return hipErrorInvalidValue;
   const size_t sl = shard_len(p.k, plen);
   const size_t tiles = (sl / 2 + TILE - 1) / TILE * batch;

@@ -686,19 +686,10 @@ bool k256_applicable(const CodeParams &p) { return p.k == 256 && (p.n == 1024 ||
 hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                               size_t sstride, hipStream_t s) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&encode_k256<1024>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&encode_k256<2048>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    if (e != hipSuccess) return e;
-  }
+  int cus = 0;
+  const void *fn = p.n == 1024 ? reinterpret_cast<const void *>(&encode_k256<1024>)
+                               : reinterpret_cast<const void *>(&encode_k256<2048>);
+  if (const hipError_t e = prepare_kernel(fn, LDS_BYTES, &cus); e != hipSuccess) return e;
   const size_t sl = shard_len(p.k, plen);
   const size_t tiles = (sl / 2 + TILE - 1) / TILE * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));

@@ -15,6 +15,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/erasure_coding/ec_amd.h"
@@ -33,30 +34,60 @@ __global__ void __launch_bounds__(256) scatter_present(const uint8_t *__restrict
                                                        uint32_t cnt, uint64_t slen,
                                                        uint8_t *__restrict__ full, uint64_t fstride,
                                                        uint32_t nv, uint8_t *__restrict__ present,
-                                                       uint32_t n) {
-  const uint32_t b = blockIdx.y, j = blockIdx.x;
-  const uint32_t v = idx[uint64_t(b) * cnt + j];
-  if (v >= nv) return;  // validated on the host; never index out of the row block
-  const uint8_t *src = compact + (uint64_t(b) * cnt + j) * cstride;
-  uint8_t *dst = full + (uint64_t(b) * nv + v) * fstride;
-  if (threadIdx.x == 0) present[uint64_t(b) * n + v] = 1;
-  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
-  const uint64_t nvec = vec ? slen / 16 : 0;
-  for (uint64_t e = threadIdx.x; e < nvec; e += blockDim.x)
-    reinterpret_cast<uint4 *>(dst)[e] = reinterpret_cast<const uint4 *>(src)[e];
-  for (uint64_t e = nvec * 16 + threadIdx.x; e < slen; e += blockDim.x) dst[e] = src[e];
+                                                       uint32_t n, uint32_t batch) {
+  const uint32_t j = blockIdx.x;
+  for (uint32_t b = blockIdx.y; b < batch; b += gridDim.y) {  // batch may exceed gridDim.y's limit
+    const uint32_t v = idx[uint64_t(b) * cnt + j];
+    if (v >= nv) continue;  // validated on the host; never index out of the row block
+    const uint8_t *src = compact + (uint64_t(b) * cnt + j) * cstride;
+    uint8_t *dst = full + (uint64_t(b) * nv + v) * fstride;
+    if (present && threadIdx.x == 0) present[uint64_t(b) * n + v] = 1;
+    const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+    const uint64_t nvec = vec ? slen / 16 : 0;
+    for (uint64_t e = threadIdx.x; e < nvec; e += blockDim.x)
+      reinterpret_cast<uint4 *>(dst)[e] = reinterpret_cast<const uint4 *>(src)[e];
+    for (uint64_t e = nvec * 16 + threadIdx.x; e < slen; e += blockDim.x) dst[e] = src[e];
+  }
 }
 
 struct Slot {
   hipStream_t stream = nullptr;
   uint8_t *d_a = nullptr, *d_b = nullptr, *d_c = nullptr, *d_present = nullptr;
   uint16_t *d_elog = nullptr, *d_idx = nullptr;
-  size_t cap_a = 0, cap_b = 0, cap_c = 0, cap_present = 0, cap_elog = 0, cap_idx = 0;
+  uint32_t *d_pat = nullptr;
+  size_t cap_a = 0, cap_b = 0, cap_c = 0, cap_present = 0, cap_elog = 0, cap_idx = 0, cap_pat = 0;
+  // host staging of a chunk's distinct erasure patterns; `staged` is recorded
+  // after their upload so the next chunk on this slot does not overwrite them early
+  std::vector<uint8_t> h_rows;
+  std::vector<uint32_t> h_pat;
+  hipEvent_t staged = nullptr;
 };
 
 struct Pipeline {
   Slot slot[kSlots];
   int device = -1;
+  ~Pipeline() { release(); }
+  // synchronise and free every slot's stream and buffers, on their own device
+  void release() {
+    if (device < 0) return;
+    int cur = -1;
+    const bool switched = hipGetDevice(&cur) == hipSuccess && cur != device &&
+                          hipSetDevice(device) == hipSuccess;
+    for (Slot &s : slot) {
+      if (s.stream) {
+        (void)hipStreamSynchronize(s.stream);
+        (void)hipStreamDestroy(s.stream);
+      }
+      if (s.staged) (void)hipEventDestroy(s.staged);
+      for (void *p : {static_cast<void *>(s.d_a), static_cast<void *>(s.d_b), static_cast<void *>(s.d_c),
+                      static_cast<void *>(s.d_present), static_cast<void *>(s.d_elog),
+                      static_cast<void *>(s.d_idx), static_cast<void *>(s.d_pat)})
+        if (p) (void)hipFree(p);
+      s = Slot{};
+    }
+    if (switched) (void)hipSetDevice(cur);
+    device = -1;
+  }
 };
 
 // chunk = 0: payloads per pipeline step such that a step moves ~16 MB over
@@ -76,11 +107,14 @@ Pipeline *pipeline() {  // one per host thread (reentrant like the reference)
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   if (pl.device != dev) {
-    for (Slot &s : pl.slot) {
-      s = Slot{};
-      if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    }
+    pl.release();  // the previous device's slots
     pl.device = dev;
+    for (Slot &s : pl.slot)
+      if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&s.staged, hipEventDisableTiming) != hipSuccess) {
+        pl.release();
+        return nullptr;
+      }
   }
   return &pl;
 }
@@ -104,6 +138,13 @@ NPRSResult res(NPRSResult_Tag t) {
 }
 
 size_t round16(size_t x) { return (x + 15) / 16 * 16; }
+
+uint64_t mix64(uint64_t x) {  // splitmix64 finaliser (pattern hash terms)
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
 
 }  // namespace
 }  // namespace ecamd
@@ -149,6 +190,7 @@ NPRSResult ECCR_AMD_encode_host_batch(unsigned long nv, const uint8_t *h_payload
     if (!grow(&s.d_a, &s.cap_a, chunk * dps) || !grow(&s.d_b, &s.cap_b, chunk * nv * dss))
       return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
     ScratchLease lease(d, encode_scratch_bytes(p, plen, cb), s.stream);  // slots never share it concurrently
+    if (!lease.ok()) return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
     void *scratch = lease.ptr();
     const uint8_t *hp = h_payloads + c0 * pstride;
     uint8_t *hs = h_shards + c0 * nv * sstride;
@@ -186,9 +228,14 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
   if (cnt < p.k) return res(NPRS_RESULT_NOT_ENOUGH_CHUNKS);  // reed-solomon.hpp:99-100
   // src/erasure_coding.rs:370-375 (index bounds) and reed-solomon.hpp:99-100
   // (enough distinct shards; a repeated index counts once, its rows must agree)
+  // per payload: its erasure pattern's hash (sum of mix64 over the distinct
+  // present indices) and size, for the per-chunk pattern dedup below
   std::vector<uint32_t> seen(nv, 0);
+  std::vector<uint64_t> phash(batch);
+  std::vector<uint32_t> pcount(batch);
   for (unsigned long b = 0; b < batch; ++b) {
     unsigned long distinct = 0;
+    uint64_t h = 0;
     for (unsigned long j = 0; j < cnt; ++j) {
       const uint16_t v = h_index[b * cnt + j];
       if (v >= nv) {
@@ -200,9 +247,12 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
       if (seen[v] != b + 1) {
         seen[v] = uint32_t(b + 1);
         ++distinct;
+        h += mix64(v);
       }
     }
     if (distinct < p.k) return res(NPRS_RESULT_NOT_ENOUGH_CHUNKS);
+    phash[b] = h;
+    pcount[b] = uint32_t(distinct);
   }
   DeviceState *d = device_state();
   const uint16_t *fold = d ? device_fold(d, p.n) : nullptr;
@@ -218,9 +268,46 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
     if (!grow(&s.d_a, &s.cap_a, chunk * cnt * sstride) || !grow(&s.d_b, &s.cap_b, chunk * nv * dss) ||
         !grow(&s.d_c, &s.cap_c, chunk * dos) || !grow(&s.d_present, &s.cap_present, chunk * p.n) ||
         !grow(&s.d_elog, &s.cap_elog, chunk * p.n * 2) ||
-        !grow(&s.d_idx, &s.cap_idx, chunk * cnt * 2))
+        !grow(&s.d_idx, &s.cap_idx, chunk * cnt * 2) || !grow(&s.d_pat, &s.cap_pat, chunk * 4))
       return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+    // distinct erasure patterns of the chunk: one present
+    // row and one locator each; payload b uses row h_pat[b]
+    if (!ok(hipEventSynchronize(s.staged), "staging reuse")) return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+    s.h_pat.resize(cb);
+    s.h_rows.clear();
+    std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;
+    std::vector<uint32_t> pat_count;  // distinct indices per pattern
+    uint32_t npat = 0;
+    for (size_t j = 0; j < cb; ++j) {
+      const size_t b = c0 + j;
+      const uint16_t *ix = h_index + b * cnt;
+      if (j > 0 && std::memcmp(ix, ix - cnt, cnt * 2) == 0) {  // same list as the previous payload
+        s.h_pat[j] = s.h_pat[j - 1];
+        continue;
+      }
+      int32_t found = -1;
+      auto &cands = by_hash[phash[b]];
+      for (uint32_t q : cands) {  // equal sets: same size and every index of b in q's row
+        const uint8_t *row = s.h_rows.data() + size_t(q) * p.n;
+        bool same = pat_count[q] == pcount[b];
+        for (unsigned long t = 0; t < cnt && same; ++t) same = row[ix[t]] != 0;
+        if (same) {
+          found = int32_t(q);
+          break;
+        }
+      }
+      if (found < 0) {
+        found = int32_t(npat++);
+        cands.push_back(uint32_t(found));
+        pat_count.push_back(pcount[b]);
+        s.h_rows.resize(size_t(npat) * p.n, 0);
+        uint8_t *row = s.h_rows.data() + size_t(found) * p.n;
+        for (unsigned long t = 0; t < cnt; ++t) row[ix[t]] = 1;
+      }
+      s.h_pat[j] = uint32_t(found);
+    }
     ScratchLease lease(d, reconstruct_scratch_bytes(p, slen, cb), s.stream);  // slots never share it concurrently
+    if (!lease.ok()) return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
     void *scratch = lease.ptr();
     bool good =
         ok(hipMemcpyAsync(s.d_a, h_shards + c0 * cnt * sstride, cb * cnt * sstride,
@@ -229,16 +316,22 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
         ok(hipMemcpyAsync(s.d_idx, h_index + c0 * cnt, cb * cnt * 2, hipMemcpyHostToDevice,
                           s.stream),
            "H2D index") &&
-        ok(hipMemsetAsync(s.d_present, 0, cb * p.n, s.stream), "present reset");
+        ok(hipMemcpyAsync(s.d_present, s.h_rows.data(), size_t(npat) * p.n, hipMemcpyHostToDevice,
+                          s.stream),
+           "H2D patterns") &&
+        ok(hipMemcpyAsync(s.d_pat, s.h_pat.data(), cb * 4, hipMemcpyHostToDevice, s.stream),
+           "H2D pattern index") &&
+        ok(hipEventRecord(s.staged, s.stream), "staging event");
     if (good) {
-      hipLaunchKernelGGL(scatter_present, dim3(unsigned(cnt), unsigned(cb)), dim3(256), 0, s.stream,
-                         s.d_a, uint64_t(sstride), s.d_idx, uint32_t(cnt), uint64_t(slen), s.d_b,
-                         uint64_t(dss), uint32_t(nv), s.d_present, uint32_t(p.n));
+      hipLaunchKernelGGL(scatter_present, dim3(unsigned(cnt), unsigned(cb < 65535 ? cb : 65535)), dim3(256),
+                         0, s.stream, s.d_a, uint64_t(sstride), s.d_idx, uint32_t(cnt), uint64_t(slen),
+                         s.d_b, uint64_t(dss), uint32_t(nv), static_cast<uint8_t *>(nullptr),
+                         uint32_t(p.n), uint32_t(cb));
       good = ok(hipGetLastError(), "scatter launch") &&
-             ok(launch_error_locator(p, s.d_present, cb, fold, s.d_elog, nullptr, s.stream),
+             ok(launch_error_locator(p, s.d_present, npat, fold, nullptr, s.d_elog, s.stream),
                 "error locator launch") &&
-             ok(launch_reconstruct(p, device_tables(d), s.d_b, slen, dss, s.d_present, s.d_elog, cb,
-                                   s.d_c, dos, scratch, s.stream),
+             ok(launch_reconstruct(p, device_tables(d), s.d_b, slen, dss, s.d_present, s.d_elog,
+                                   s.d_pat, cb, s.d_c, dos, scratch, s.stream),
                 "reconstruct launch") &&
              ok(out_lin ? hipMemcpyAsync(h_out + c0 * ostride, s.d_c, (cb - 1) * ostride + ob,
                                          hipMemcpyDeviceToHost, s.stream)

@@ -117,6 +117,11 @@ def lib():
             "ECCR_AMD_error_locator": (NPRSResult, [ul, vp, ul, vp, vp]),
             "ECCR_AMD_reconstruct_batch": (NPRSResult, [ul, vp, ul, ul, vp, vp, ul, vp, ul, vp]),
             "ECCR_AMD_systematic_batch": (NPRSResult, [ul, vp, ul, ul, ul, vp, ul, vp]),
+            "ECCR_AMD_dedup_patterns": (NPRSResult, [ul, vp, ul, vp, vp]),
+            "ECCR_AMD_error_locator_patterns": (NPRSResult, [ul, vp, vp, ul, vp, vp]),
+            "ECCR_AMD_reconstruct_batch_patterns": (NPRSResult, [ul, vp, ul, ul, vp, vp, vp, ul, vp,
+                                                                 ul, vp]),
+            "ECCR_AMD_locator_cache_stats": (NPRSResult, [up, up]),
             "ECCR_AMD_host_alloc": (vp, [ul]),
             "ECCR_AMD_host_free": (None, [vp]),
             "ECCR_AMD_encode_host_batch": (NPRSResult, [ul, vp, ul, ul, ul, vp, ul, ul]),
@@ -270,6 +275,34 @@ def reconstruct_batch(nv, d_shards, shard_len_, shard_stride, d_present, d_err_l
                                             _p(d_present), _p(d_err_log), batch, _p(d_out),
                                             out_stride, _stream(stream)),
            "reconstruct_batch")
+
+
+def dedup_patterns(nv, d_present, batch, d_pattern, stream=None):
+    """d_pattern[b] (uint32) = smallest index with the same erasure pattern as b."""
+    _check(lib().ECCR_AMD_dedup_patterns(nv, _p(d_present), batch, _p(d_pattern), _stream(stream)),
+           "dedup_patterns")
+
+
+def error_locator_patterns(nv, d_present, d_pattern, batch, d_err_log, stream=None):
+    _check(lib().ECCR_AMD_error_locator_patterns(nv, _p(d_present),
+                                                 None if d_pattern is None else _p(d_pattern),
+                                                 batch, _p(d_err_log), _stream(stream)),
+           "error_locator_patterns")
+
+
+def reconstruct_batch_patterns(nv, d_shards, shard_len_, shard_stride, d_present, d_err_log,
+                               d_pattern, batch, d_out, out_stride, stream=None):
+    """reconstruct_batch where payload b uses row d_pattern[b] of d_present / d_err_log."""
+    _check(lib().ECCR_AMD_reconstruct_batch_patterns(
+        nv, _p(d_shards), shard_len_, shard_stride, _p(d_present), _p(d_err_log),
+        None if d_pattern is None else _p(d_pattern), batch, _p(d_out), out_stride,
+        _stream(stream)), "reconstruct_batch_patterns")
+
+
+def locator_cache_stats():
+    h, m = C.c_ulong(), C.c_ulong()
+    _check(lib().ECCR_AMD_locator_cache_stats(C.byref(h), C.byref(m)), "locator_cache_stats")
+    return h.value, m.value
 
 
 def systematic_batch(nv, d_shards, shard_len_, shard_stride, batch, d_out, out_stride, stream=None):

@@ -4,8 +4,14 @@
  *
  * All pointers named d_* are device pointers on the codec's device; `stream`
  * is a hipStream_t (NULL = the legacy default stream).  Calls are asynchronous
- * on `stream` and capture-safe (no allocation, no synchronisation): the
- * caller owns every buffer.  Results are bit-exact with ec-cpp:
+ * on `stream` and the caller owns every buffer it passes.  They are NOT
+ * graph-capture-safe in general: the first call per (device, kernel) sets a
+ * kernel attribute; shapes that need device scratch (k = 1024 encodes, n > 4096
+ * generic kernels, ECCR_AMD_error_locator / ECCR_AMD_dedup_patterns with
+ * batch > 1) take a per-device scratch buffer that may be (re)allocated with
+ * hipMalloc / hipFree and is ordered across streams with an event
+ * (hipStreamWaitEvent, and hipEventSynchronize when it grows).  Warm a shape
+ * up once outside capture.  Results are bit-exact with ec-cpp:
  *   encode      == ReedSolomon::encode      (include/ec-cpp/reed-solomon.hpp:47-81)
  *   reconstruct == ReedSolomon::reconstruct (include/ec-cpp/reed-solomon.hpp:83-134)
  *   systematic  == ReedSolomon::reconstruct_from_systematic (:143-179)
@@ -49,19 +55,54 @@ struct NPRSResult ECCR_AMD_encode_batch(unsigned long n_validators, const uint8_
                                         unsigned long batch, uint8_t *d_shards,
                                         unsigned long shard_stride, void *stream);
 
-/* Erasure-locator multipliers for a batch of erasure patterns. */
+/* Erasure-locator multipliers for a batch of erasure patterns, one row of
+ * d_err_log per row of d_present.  With batch > 1, equal patterns are found on
+ * the device (ECCR_AMD_dedup_patterns) and each distinct one is computed once,
+ * then copied to the payloads that share it. */
 struct NPRSResult ECCR_AMD_error_locator(unsigned long n_validators, const uint8_t *d_present,
                                          unsigned long batch, uint16_t *d_err_log,
                                          void *stream);
 
 /* Device-resident batch reconstruct (needs ECCR_AMD_error_locator output).
- * The caller guarantees >= k present shards per payload (the host C ABI
- * checks this); missing shards' bytes are never read. */
+ * The device path does not count shards: a payload with fewer than k present
+ * shards yields unspecified bytes (never an out-of-bounds access).  The host
+ * entry points (ECCR_reconstruct, ECCR_AMD_reconstruct_host_batch) check the
+ * count and return NOT_ENOUGH_CHUNKS.  Missing shards' bytes are never read. */
 struct NPRSResult ECCR_AMD_reconstruct_batch(unsigned long n_validators, const uint8_t *d_shards,
                                              unsigned long shard_len, unsigned long shard_stride,
                                              const uint8_t *d_present, const uint16_t *d_err_log,
                                              unsigned long batch, uint8_t *d_out,
                                              unsigned long out_stride, void *stream);
+
+/* ---- shared erasure patterns ------------------------
+ * d_pattern [batch] (uint32): payload b's erasure pattern is row d_pattern[b]
+ * of d_present / d_err_log (rows may be shared by any number of payloads;
+ * NULL = row b).  The usual case: the same validators missing for every block,
+ * i.e. ONE present row and ONE locator for the whole batch. */
+
+/* d_pattern[b] = the smallest index whose pattern (present flags of positions
+ * < n_validators) equals payload b's, over the rows of d_present [batch][n]. */
+struct NPRSResult ECCR_AMD_dedup_patterns(unsigned long n_validators, const uint8_t *d_present,
+                                          unsigned long batch, uint32_t *d_pattern, void *stream);
+
+/* Locators of the rows b with d_pattern[b] == b only (the other rows of
+ * d_err_log are left untouched; d_pattern NULL: every row). */
+struct NPRSResult ECCR_AMD_error_locator_patterns(unsigned long n_validators,
+                                                  const uint8_t *d_present,
+                                                  const uint32_t *d_pattern, unsigned long batch,
+                                                  uint16_t *d_err_log, void *stream);
+
+/* ECCR_AMD_reconstruct_batch with payload b's pattern = row d_pattern[b]. */
+struct NPRSResult ECCR_AMD_reconstruct_batch_patterns(
+    unsigned long n_validators, const uint8_t *d_shards, unsigned long shard_len,
+    unsigned long shard_stride, const uint8_t *d_present, const uint16_t *d_err_log,
+    const uint32_t *d_pattern, unsigned long batch, uint8_t *d_out, unsigned long out_stride,
+    void *stream);
+
+/* Hits / misses of the per-device locator cache of ECCR_reconstruct (the
+ * locator of a pattern is computed once and reused while it is among the 64
+ * most recent patterns). */
+struct NPRSResult ECCR_AMD_locator_cache_stats(unsigned long *hits, unsigned long *misses);
 
 /* Device-resident batch reconstruct_from_systematic (shards 0..k-1 of each
  * payload, same [batch][n_validators][shard_stride] layout). */
@@ -70,7 +111,6 @@ struct NPRSResult ECCR_AMD_systematic_batch(unsigned long n_validators, const ui
                                             unsigned long batch, uint8_t *d_out,
                                             unsigned long out_stride, void *stream);
 
-/* Last error message of the calling thread ("" if none). */
 /* ---- host-resident batches --------------------------
  * Stream a host batch through the device in chunks of `chunk` payloads (0 =
  * automatic: ~16 MB over the link per chunk), three chunks in flight (H2D /
@@ -90,6 +130,7 @@ struct NPRSResult ECCR_AMD_encode_host_batch(unsigned long n_validators, const u
 /* `count` present shards per payload, compacted: h_shards [batch][count][shard_stride]
  * with their validator indices h_index [batch][count] (a repeated index counts
  * once and must carry identical bytes) -> h_out [batch][out_stride >= shard_len*k].
+ * Payloads with the same set of indices share one erasure locator per chunk.
  * Errors as ECCR_reconstruct: CHUNK_INDEX_OUT_OF_BOUNDS, NOT_ENOUGH_CHUNKS (< k
  * distinct), UNEVEN_LENGTH. */
 struct NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long n_validators,
@@ -99,6 +140,7 @@ struct NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long n_validators,
                                                   unsigned long batch, uint8_t *h_out,
                                                   unsigned long out_stride, unsigned long chunk);
 
+/* Last error message of the calling thread ("" if none). */
 const char *ECCR_AMD_last_error(void);
 
 #ifdef __cplusplus

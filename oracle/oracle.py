@@ -222,3 +222,17 @@ class RefEC(_Lib):
         if e:
             raise CodecError(e)
         return te.value, td.value
+
+    def time_mt(self, nv: int, payload: bytes, present: np.ndarray, threads: int, seconds: float):
+        """All-core rate: `threads` threads each encoding + reconstructing the
+        payload until `seconds` pass.  Returns (payloads done, wall s, encode s
+        summed over threads, reconstruct s summed over threads)."""
+        p = np.ascontiguousarray(np.frombuffer(bytes(payload), np.uint8))
+        pr = np.ascontiguousarray(present, np.uint8)
+        done, wall, te, td = C.c_uint64(), C.c_double(), C.c_double(), C.c_double()
+        e = self.lib.ecref_time_mt(C.c_size_t(nv), _ptr(p), C.c_size_t(p.size), _ptr(pr),
+                                   C.c_int(threads), C.c_double(seconds), C.byref(done),
+                                   C.byref(wall), C.byref(te), C.byref(td))
+        if e:
+            raise CodecError(e)
+        return done.value, wall.value, te.value, td.value

@@ -6,9 +6,11 @@
 // baseline.  The output library lives in oracle/_ref/ (git-ignored).  This
 // file contains no reference source; it only calls the reference API
 // (include/ec-cpp/ec-cpp.hpp:15-26, reed-solomon.hpp:47-179).
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include <ec-cpp/ec-cpp.hpp>
@@ -130,6 +132,47 @@ int ecref_time(size_t nv, const uint8_t *p, size_t len, const uint8_t *present,
   *sec_enc = std::chrono::duration<double>(t1 - t0).count();
   *sec_dec = std::chrono::duration<double>(t3 - t2).count();
   return 0;
+}
+
+// All-core rate: `threads` threads, each encoding the payload
+// and reconstructing it from the shards flagged present, one payload per
+// thread at a time, until `seconds` have passed (ec-cpp's thread_local
+// scratch, reed-solomon.hpp:198-201, makes concurrent calls safe).  *done =
+// payloads completed by all threads; *wall = elapsed seconds; *enc / *dec =
+// encode / reconstruct seconds summed over the threads.
+int ecref_time_mt(size_t nv, const uint8_t *p, size_t len, const uint8_t *present, int threads,
+                  double seconds, uint64_t *done, double *wall, double *enc, double *dec) {
+  using clk = std::chrono::steady_clock;
+  std::atomic<uint64_t> count{0};
+  std::atomic<int> err{0};
+  std::vector<double> te(threads, 0.0), td(threads, 0.0);
+  const auto t0 = clk::now();
+  const auto stop = t0 + std::chrono::duration<double>(seconds);
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; ++t)
+    pool.emplace_back([&, t] {
+      std::vector<uint8_t> mine(p, p + len);  // each thread its own input
+      do {
+        double a = 0, b = 0;
+        const int e = ecref_time(nv, mine.data(), len, present, &a, &b);
+        if (e) {
+          err = e;
+          return;
+        }
+        te[t] += a;
+        td[t] += b;
+        ++count;
+      } while (clk::now() < stop);
+    });
+  for (auto &th : pool) th.join();
+  *wall = std::chrono::duration<double>(clk::now() - t0).count();
+  *done = count.load();
+  *enc = *dec = 0;
+  for (int t = 0; t < threads; ++t) {
+    *enc += te[t];
+    *dec += td[t];
+  }
+  return err.load();
 }
 
 }  // extern "C"

@@ -291,3 +291,202 @@ def test_capi_concurrent_threads(oracle):
         t.join(120)
     assert not any(t.is_alive() for t in threads)
     assert not errors, errors
+
+
+# ------------------------------------------- erasure patterns per reconstruct kernel
+def _pattern_rows(nv, n, k, thr, rng):
+    """One present mask per pattern the reference's gap / erased-index handling
+    distinguishes (reed-solomon.hpp:83-134): exactly k, threshold, every shard
+    (E == 0 erasures), all systematic rows present with some y >= k erased,
+    only the systematic rows, only non-systematic rows."""
+    rows = {}
+
+    def mask(idx):
+        m = np.zeros(n, dtype=np.uint8)
+        m[np.asarray(sorted(idx), dtype=np.int64)] = 1
+        return m
+
+    rows["k"] = mask(rng.permutation(nv)[:k])
+    rows["threshold"] = mask(rng.permutation(nv)[:thr])
+    rows["all"] = mask(range(nv))
+    if nv > k:
+        extra = rng.permutation(np.arange(k, nv))[: max(1, (nv - k) // 2)]
+        rows["systematic+some"] = mask(list(range(k)) + [int(x) for x in extra])
+        rows["systematic_only"] = mask(range(k))
+    if nv - k >= k:
+        rows["parity_only"] = mask(k + rng.permutation(nv - k)[:k])
+    return rows
+
+
+def _prefilled(shape, fill=0xAA):
+    import torch
+    return torch.full(shape, fill, dtype=torch.uint8, device="cuda")
+
+
+@pytest.mark.parametrize("nv,plen,pad", [
+    (1024, 70001, 64), (800, 33333, 16),                # reconstruct_n1024 (nv = n and nv < n)
+    (1500, 70001, 64), (2048, 40001, 16),               # reconstruct_n4096, 2 halves, k = 256 / 512
+    (2500, 70001, 64), (3070, 90001, 16), (4096, 70001, 64),  # 4 quarters, k = 512 / 1024
+    (600, 50001, 64), (300, 20001, 16), (100, 9999, 16), (46, 5001, 64),  # reconstruct_gen
+    (6, 3001, 0), (20, 999, 0), (5000, 40001, 0)])     # generic kernels (incl. n = 8192)
+def test_batch_patterns_every_kernel(oracle, nv, plen, pad):
+    """Device batch reconstruct through ECCR_AMD_reconstruct_batch with every
+    pattern class, outputs and shard padding prefilled with 0xAA (a missed
+    write or a read of an absent row shows up), compared with the oracle."""
+    import torch
+    n, k, thr = E.code_params(nv)
+    rng = np.random.default_rng(nv * 7 + plen)
+    rows = _pattern_rows(nv, n, k, thr, rng)
+    names = list(rows)
+    batch = len(names)
+    sl = E.shard_len(nv, plen)
+    ss = (sl + pad - 1) // pad * pad if pad else sl
+    pay = np.stack([synth.payload(9000 + nv + b, plen) for b in range(batch)])
+    pres = np.stack([rows[x] for x in names])
+    d_pay = torch.from_numpy(pay).cuda()
+    d_sh = _prefilled((batch, nv, ss))
+    d_pr = torch.from_numpy(pres).cuda()
+    d_el = torch.zeros((batch, n), dtype=torch.int16, device="cuda")
+    d_out = _prefilled((batch, sl * k))
+    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+    torch.cuda.synchronize()
+    # absent shards: garbage bytes (must never be read)
+    sh_np = d_sh.cpu().numpy()
+    for b in range(batch):
+        gone = np.where(pres[b][:nv] == 0)[0]
+        d_sh[b, torch.from_numpy(gone).cuda()] = 0x5C
+    E.error_locator(nv, d_pr, batch, d_el)
+    E.reconstruct_batch(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    for b, name in enumerate(names):
+        ref = oracle.encode(nv, pay[b].tobytes())
+        assert b"".join(ref) == sh_np[b][:, :sl].tobytes(), (name, "encode")
+        keep = [ref[i] if pres[b][i] else None for i in range(nv)]
+        assert out[b].tobytes() == oracle.reconstruct(nv, keep), name
+        assert out[b][:plen].tobytes() == pay[b].tobytes(), name
+
+
+@pytest.mark.parametrize("nv,plen,pad", [(1024, 40001, 64), (600, 30001, 64), (4096, 50001, 64),
+                                         (1500, 30001, 16), (20, 999, 0)])
+def test_shared_patterns(oracle, nv, plen, pad):
+    """Per-pattern locator dedup: many payloads share a
+    few erasure patterns.  ECCR_AMD_error_locator computes each distinct one
+    once (its rows still equal oracle.error_poly), ECCR_AMD_dedup_patterns
+    finds the leaders, and ECCR_AMD_reconstruct_batch_patterns reads the shared
+    rows; every output equals the oracle's."""
+    import torch
+    n, k, thr = E.code_params(nv)
+    base = [synth.present_mask(77 + j, nv, thr, n) for j in range(3)]
+    # same sets also arrive as bytes other than 1 and with flags past nv set
+    alt = base[1].copy()
+    alt[alt == 1] = 7
+    if n > nv:
+        alt[nv:] = 1
+    which = [0, 1, 0, 0, 2, 1, 2, 0, 1, 0, 0, 2]
+    batch = len(which)
+    pres = np.stack([alt if (w == 1 and b % 2) else base[w] for b, w in enumerate(which)])
+    d_pr = torch.from_numpy(pres).cuda()
+    d_el = torch.zeros((batch, n), dtype=torch.int16, device="cuda")
+    E.error_locator(nv, d_pr, batch, d_el)
+    d_pat = torch.zeros(batch, dtype=torch.int32, device="cuda")
+    E.dedup_patterns(nv, d_pr, batch, d_pat)
+    torch.cuda.synchronize()
+    el = d_el.cpu().numpy().view(np.uint16)
+    first = {}
+    want = [first.setdefault(w, b) for b, w in enumerate(which)]
+    assert d_pat.cpu().numpy().tolist() == want
+    for b in range(batch):
+        erased = (pres[b][:n] == 0).astype(np.uint8)
+        erased[nv:] = 1
+        ep = oracle.error_poly(erased, n)[:n].astype(np.int64) % 65535
+        assert ((el[b].astype(np.int64) % 65535) == ep).all(), b
+    # reconstruct with ONE present row / locator per distinct pattern
+    sl = E.shard_len(nv, plen)
+    ss = (sl + pad - 1) // pad * pad if pad else sl
+    pay = np.stack([synth.payload(4000 + b, plen) for b in range(batch)])
+    d_pay = torch.from_numpy(pay).cuda()
+    d_sh = _prefilled((batch, nv, ss))
+    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+    d_rows = torch.from_numpy(np.stack(base)).cuda()
+    d_rel = torch.zeros((3, n), dtype=torch.int16, device="cuda")
+    E.error_locator_patterns(nv, d_rows, None, 3, d_rel)
+    d_idx = torch.tensor(which, dtype=torch.int32, device="cuda")
+    d_out = _prefilled((batch, sl * k))
+    E.reconstruct_batch_patterns(nv, d_sh, sl, ss, d_rows, d_rel, d_idx, batch, d_out, sl * k)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    sh = d_sh.cpu().numpy()[:, :, :sl]
+    for b, w in enumerate(which):
+        shards = [sh[b][i].tobytes() for i in range(nv)]
+        keep = [shards[i] if base[w][i] else None for i in range(nv)]
+        assert out[b].tobytes() == oracle.reconstruct(nv, keep), b
+
+
+def test_locator_cache_per_call(oracle):
+    """ECCR_reconstruct computes a pattern's locator once per device and then
+    reuses it (the same validators missing for every block)."""
+    nv = 1024
+    n, k, thr = E.code_params(nv)
+    keep = set(int(x) for x in synth.present_set(31337, nv, thr))
+    h0, m0 = E.locator_cache_stats()
+    for rep in range(4):
+        p = synth.payload(600 + rep, 20000 + rep).tobytes()
+        sh = E.obtain_chunks(nv, p)
+        out = decode_subset(nv, sh, keep)
+        assert out == oracle.reconstruct(nv, [sh[i] if i in keep else None for i in range(nv)])
+    h1, m1 = E.locator_cache_stats()
+    assert m1 - m0 == 1 and h1 - h0 == 3
+
+
+# ----------------------------------------- host batches at the config-5 sizes (row f2)
+README_SIZES = [15, 300, 5000, 100_000, 1_000_000, 10_000_000]  # README.md:50-84
+
+
+def _host_roundtrip(oracle, nv, plen, batch, chunk, seed, shared=False, check_all=True):
+    n, k, thr = E.code_params(nv)
+    sl = E.shard_len(nv, plen)
+    pay = np.stack([synth.payload(seed + b, plen) for b in range(batch)])
+    sh = np.full((batch, nv, sl), 0xAA, dtype=np.uint8)
+    E.encode_host_batch(nv, pay, plen, plen, batch, sh, sl, chunk)
+    for b in (range(batch) if check_all else [0, batch - 1]):
+        assert b"".join(oracle.encode(nv, pay[b].tobytes())) == sh[b].tobytes(), (plen, b)
+    if shared:  # one validator set for every payload, listed in different orders
+        s0 = synth.present_set(seed, nv, thr)
+        idx = np.stack([np.random.default_rng(b).permutation(s0) for b in range(batch)]).astype(np.uint16)
+    else:
+        idx = np.stack([synth.present_set(seed + 7 * b, nv, thr) for b in range(batch)]).astype(np.uint16)
+    comp = np.stack([sh[b][idx[b]] for b in range(batch)])
+    out = np.full((batch, sl * k), 0xAA, dtype=np.uint8)
+    E.reconstruct_host_batch(nv, comp, sl, sl, idx, thr, batch, out, sl * k, chunk)
+    for b in range(batch):
+        assert out[b][:plen].tobytes() == pay[b].tobytes(), (plen, b)
+        assert not out[b][plen:].any(), (plen, b)
+    for b in (range(batch) if check_all else [0]):
+        kk = set(int(x) for x in idx[b])
+        keep = [sh[b][i].tobytes() if i in kk else None for i in range(nv)]
+        assert out[b].tobytes() == oracle.reconstruct(nv, keep), (plen, b)
+
+
+@pytest.mark.parametrize("plen,batch", [(15, 300), (300, 100), (10_000_000, 2)])
+def test_host_batch_config5_sizes(oracle, plen, batch):
+    """The 15 B, 300 B and 10 MB classes of the config-5 stream through the
+    host-batch pipeline with automatic chunking (chunk = 0), nv = 1024."""
+    _host_roundtrip(oracle, 1024, plen, batch, 0, seed=plen, check_all=plen < 10_000_000)
+
+
+def test_host_batch_shared_patterns(oracle):
+    """Every payload of the host batch has the same validator set (in different
+    orders): one locator per chunk, results unchanged."""
+    _host_roundtrip(oracle, 1024, 5000, 40, 0, seed=17, shared=True)
+    _host_roundtrip(oracle, 600, 5000, 9, 4, seed=18, shared=True)
+
+
+def test_host_batch_mixed_stream(oracle):
+    """Config 5 shape on one GPU: the six README sizes round-robin through the
+    host-batch pipeline (chunk = 0), every result checked."""
+    for rnd in range(2):
+        for j, plen in enumerate(README_SIZES):
+            batch = {15: 64, 300: 32, 5000: 16, 100_000: 8, 1_000_000: 3, 10_000_000: 1}[plen]
+            _host_roundtrip(oracle, 1024, plen, batch, 0, seed=1000 * rnd + j,
+                            check_all=plen <= 100_000)
