@@ -111,6 +111,71 @@ def cpu_baseline(nv, plen, cnt, seconds):
     return res
 
 
+def scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out, step_s, timeout_s):
+    """SURVEY.md §8e / north_star: the batch starts on GPU0 and the decoded
+    payloads end there.  Rank 0 holds every rank's payloads, scatters them over
+    RCCL (one grouped batch of ncclSend / ncclRecv: each rank's slice on its own
+    xGMI link), and the reconstructed payloads are gathered back.  Timed apart
+    from the device-resident step (barrier + synchronize around each phase, max
+    over ranks) and checked: the scattered slices equal each rank's own
+    payloads, the gathered outputs equal the root's copy of every payload."""
+    import threading
+    done = threading.Event()
+
+    def watchdog():  # a hung collective must not cost the main measurement
+        if not done.wait(timeout_s):
+            print(json.dumps({"scatter_gather_timeout_s": timeout_s}), file=sys.stderr, flush=True)
+            os._exit(3)
+
+    threading.Thread(target=watchdog, daemon=True).start()
+    whole = None
+    if rank == 0:
+        whole = torch.empty((world, B, plen), dtype=torch.uint8, device=dev)
+        for r in range(world):
+            seeds = sharding.rank_seeds(r, B)
+            for c0 in range(0, B, 256):
+                whole[r, c0:c0 + 256] = synth.payloads_torch(seeds[c0:c0 + 256], plen, device=dev)
+    recv = torch.empty((B, plen), dtype=torch.uint8, device=dev)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    def timed(fn):
+        sync()
+        dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        fn()
+        sync()
+        t1 = time.perf_counter()
+        dist.barrier()
+        return sharding.max_over_ranks(t1 - t0, dist, dev)
+
+    t_sc = timed(lambda: sharding.scatter_from_root(dist, whole, recv, rank, world))
+    ok = int(torch.equal(recv, d_pay))
+    del recv
+    ob = d_out.shape[1]
+    gath = torch.empty((world, B, ob), dtype=torch.uint8, device=dev) if rank == 0 else None
+    t_ga = timed(lambda: sharding.gather_to_root(dist, d_out, gath, rank, world))
+    if rank == 0:
+        for r in range(world):
+            ok &= int(torch.equal(gath[r, :, :plen], whole[r]))
+        del gath, whole
+    flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    done.set()
+    sc_bytes = (world - 1) * B * plen
+    ga_bytes = (world - 1) * B * ob
+    return {"scatter_ms": round(t_sc * 1e3, 3), "scatter_bytes": sc_bytes,
+            "scatter_GBps": round(sc_bytes / t_sc / 1e9, 2),
+            "gather_ms": round(t_ga * 1e3, 3), "gather_bytes": ga_bytes,
+            "gather_GBps": round(ga_bytes / t_ga / 1e9, 2),
+            "rate_incl_scatter_gather_GiBps": round(world * B * plen / (t_sc + step_s + t_ga) / 2**30, 3),
+            "collective": "RCCL grouped ncclSend/ncclRecv (torch.distributed batch_isend_irecv)",
+            "ok": bool(flag.item())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,6 +188,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="CPU baseline sample per leg (1 thread, all cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-scatter", action="store_true",
+                    help="skip the RCCL scatter / gather phase (N > 1)")
+    ap.add_argument("--scatter-timeout", type=float, default=180.0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -229,6 +297,9 @@ def main():
         "reconstruct_GiBps": round(world * B * plen / ((t_loc + t_rec) * 1e-3) / 2**30, 3),
         "roundtrip_ok": ok,
     }
+    if dist and backend == "nccl" and not args.no_scatter:
+        line["scatter_gather"] = scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out,
+                                                elapsed / args.steps, args.scatter_timeout)
     if rank == 0:
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(nv, plen, cnt, args.cpu_seconds)

@@ -1,8 +1,11 @@
 """Payload sharding across ranks (one process per GPU) — SURVEY.md §8e.
 
 Payloads are independent, so the multi-GPU path is a partition of the payload
-set with no data-path collective; RCCL (or gloo in the CPU tests) carries only
-the barrier and the max-over-ranks timing.
+set with no data-path collective; RCCL (or gloo in the CPU tests) carries the
+barrier and the max-over-ranks timing, and -- only when a batch starts or ends
+on one GPU -- the trivial scatter / gather below (grouped point-to-point sends
+and receives: ncclGroupStart; ncclSend / ncclRecv; ncclGroupEnd under RCCL,
+each rank's slice on its own xGMI link from the root).
 
 * weak scaling (bench.py): every rank owns `per_rank` payloads whose synthetic
   seeds are global payload indices, so the data a payload gets does not depend
@@ -53,3 +56,43 @@ def max_over_ranks(value: float, dist=None, device=None) -> float:
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def scatter_from_root(dist, src, dst, rank: int, world: int, root: int = 0) -> None:
+    """Root sends slice r of `src` ([world][...]; only read on the root) to rank
+    r; every rank (root included) receives its slice into `dst`.  One grouped
+    batch of point-to-point ops, so the root's sends run concurrently."""
+    if world == 1:
+        dst.copy_(src[0])
+        return
+    ops = []
+    if rank == root:
+        for r in range(world):
+            if r != root:
+                ops.append(dist.P2POp(dist.isend, src[r], r))
+    else:
+        ops.append(dist.P2POp(dist.irecv, dst, root))
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    if rank == root and dst.data_ptr() != src[root].data_ptr():
+        dst.copy_(src[root])
+
+
+def gather_to_root(dist, src, dst, rank: int, world: int, root: int = 0) -> None:
+    """Inverse of scatter_from_root: rank r's `src` lands in dst[r] on the root
+    (`dst` [world][...] is only written on the root)."""
+    if world == 1:
+        dst[0].copy_(src)
+        return
+    ops = []
+    if rank == root:
+        for r in range(world):
+            if r != root:
+                ops.append(dist.P2POp(dist.irecv, dst[r], r))
+    else:
+        ops.append(dist.P2POp(dist.isend, src, root))
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    if rank == root and dst[root].data_ptr() != src.data_ptr():
+        dst[root].copy_(src)
+

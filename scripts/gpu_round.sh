@@ -20,6 +20,8 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; ok $rc || exit $rc ;;
     bench_small) step bench_small 600 python bench.py --batch 512 --steps 3 --warmup 1 --cpu-seconds 3; rc=$?; ok $rc || exit $rc ;;
     bench) step bench 900 python bench.py; rc=$?; ok $rc || exit $rc ;;
+    stream) step stream 600 python scripts/bench_stream.py; rc=$?; ok $rc || exit $rc ;;
+    e2e) step e2e 600 python scripts/bench_e2e.py; rc=$?; ok $rc || exit $rc ;;
     # profiles of the default bench workload (same kernels/sizes as `python bench.py`)
     prof) step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline; rc=$?; ok $rc || exit $rc ;;
     pmc_fetch) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1; rc=$?; ok $rc || exit $rc ;;

@@ -100,3 +100,107 @@ def test_balanced_partition_deterministic():
     a = sharding.balanced_partition(MIXED, 4)
     assert a == sharding.balanced_partition(list(MIXED), 4)
     assert sorted(i for p in a for i in p) == list(range(len(MIXED)))
+
+
+def _sg_worker(rank, world, port, q):
+    """gloo rehearsal of bench.py's scatter / gather (the RCCL path runs the
+    same calls on GPU tensors): the root holds every rank's payloads, scatters
+    them, each rank encodes + reconstructs its slice on the CPU oracle, and the
+    decoded payloads are gathered back to the root."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import oracle as orc
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        per, plen, nv = 2, 777, 6
+        o = orc.Oracle()
+        n, k = o.params(nv)
+        sl = o.shard_len(k, plen)
+        whole = None
+        if rank == 0:
+            seeds = [s for r in range(world) for s in sharding.rank_seeds(r, per)]
+            whole = torch.from_numpy(np.stack([synth.payload(s, plen) for s in seeds])).view(world, per, plen)
+        mine = torch.empty((per, plen), dtype=torch.uint8)
+        sharding.scatter_from_root(dist, whole, mine, rank, world)
+        want = np.stack([synth.payload(s, plen) for s in sharding.rank_seeds(rank, per)])
+        ok_scatter = bool((mine.numpy() == want).all())
+        dec = []
+        for b in range(per):
+            sh = o.encode(nv, mine[b].numpy().tobytes())
+            keep = [sh[i] if i % 2 == 0 else None for i in range(nv)]
+            dec.append(np.frombuffer(o.reconstruct(nv, keep), np.uint8))
+        dec = torch.from_numpy(np.stack(dec))
+        assert dec.shape == (per, sl * k)
+        gathered = torch.zeros((world, per, sl * k), dtype=torch.uint8) if rank == 0 else None
+        sharding.gather_to_root(dist, dec, gathered, rank, world)
+        oks = [None] * world
+        dist.all_gather_object(oks, ok_scatter)
+        if rank == 0:
+            ok_gather = bool((gathered[:, :, :plen].reshape(world * per, plen) ==
+                              whole.reshape(world * per, plen)).all())
+            q.put((oks, ok_gather))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_scatter_gather_rehearsal(world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sg_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        oks, ok_gather = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(oks) and ok_gather
+
+
+def _bench_sg_worker(rank, world, port, q):
+    """bench.py's scatter_gather() itself, on gloo with CPU tensors (the box
+    runs it on RCCL with device tensors): payloads scattered from the root,
+    outputs gathered back, checked, timed."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        B, plen, ob = 3, 1001, 1024
+        dev = torch.device("cpu")
+        d_pay = synth.payloads_torch(sharding.rank_seeds(rank, B), plen, device=dev).contiguous()
+        d_out = torch.zeros((B, ob), dtype=torch.uint8)
+        d_out[:, :plen] = d_pay  # a correct reconstruction
+        r = bench.scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out, 1e-3, 120.0)
+        if rank == 0:
+            q.put(r)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_scatter_gather_gloo():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, port = 2, _free_port()
+    procs = [ctx.Process(target=_bench_sg_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        r = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert r["ok"] and r["scatter_bytes"] == 3 * 1001 and r["gather_bytes"] == 3 * 1024
+
