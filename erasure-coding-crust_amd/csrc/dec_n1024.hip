@@ -186,10 +186,10 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
   uint8_t *regions = lds + TAB_REGION;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t tid0 = threadIdx.x, wave = tid0 >> 6;
   uint8_t *my = regions + wave * REG_BYTES;
 
-  Tabs::fill(tabs, t.mtab, 1023, [&](uint32_t i) { return uint32_t(t.skews[i]); }, tid, THREADS);
+  Tabs::fill(tabs, t.mtab, 1023, [&](uint32_t i) { return uint32_t(t.skews[i]); }, tid0, THREADS);
   __syncthreads();
 #ifdef DEC_STAMP
   uint64_t st_ = __builtin_amdgcn_s_memtime(), acc_[11] = {};
@@ -202,7 +202,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   // present (and < nv), bits 0-15 = mul_index(E[v]).  Loaded one tile ahead so
   // the gather's table loads and the output-table fill wait on one global
   // latency instead of two (present/E, then the table).
-  auto load_meta = [&](uint64_t tl, uint32_t (&m)[2]) {
+  auto load_meta = [&](uint64_t tl, uint32_t tid, uint32_t (&m)[2]) {
     const uint64_t bb = tl / tiles_pp, pt = pattern ? pattern[bb] : bb;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -212,8 +212,14 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     }
   };
   uint32_t meta[2] = {0, 0}, meta_next[2] = {0, 0};
-  if (blockIdx.x < total) load_meta(blockIdx.x, meta);
+  if (blockIdx.x < total) load_meta(blockIdx.x, tid0, meta);
   for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    // lane-derived addresses are recomputed per tile from an opaque copy of
+    // the thread id (hoisted out of the loop they were kept live, and spilled,
+    // across the whole tile)
+    uint32_t tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const uint32_t lane = tid & 63;
     const uint64_t b = tile / tiles_pp;
     const uint64_t col0 = (tile % tiles_pp) * COLS;
     const uint64_t pt = pattern ? pattern[b] : b;  // erasure pattern of payload b
@@ -269,7 +275,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       for (int g = 0; g < 8; ++g)
         *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l[g], h[g]);
     }
-    if (tile + gridDim.x < total) load_meta(tile + gridDim.x, meta_next);
+    if (tile + gridDim.x < total) load_meta(tile + gridDim.x, tid, meta_next);
     STAMP(2);
     __syncthreads();
     STAMP(3);
@@ -315,67 +321,59 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       s.l[r] = x.x;
       s.h[r] = x.y;
     }
+    // IFFT stages 8 and 9 (inverse_afft, additive_fft.hpp:99-119, index 0).  A
+    // stage's block at j = d has skew skews[d - 1] = 0xFFFF, i.e. no multiply:
+    // stage 9 is b ^= a only, stage 8 multiplies in its p9 = 1 block only.  The
+    // p8 = p9 = 1 registers (4 hi + 3) are not needed past stage 8.
     {
-      Tab Ta, Tb;  // stage 8: skew depends on p9 only; stage 9: one skew
-      tab_at(tabs, tlin(skew_idx(0, 8)), Ta);
+      Tab Tb;
       tab_at(tabs, tlin(skew_idx(1u << 9, 8)), Tb);
 #pragma unroll
-      for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi, 4 * hi + 1, Ta);
-      tab_at(tabs, tlin(skew_idx(0, 9)), Ta);
+      for (int hi = 0; hi < 4; ++hi) {
+        s.l[4 * hi + 1] ^= s.l[4 * hi];  // stage 8, p9 = 0 block
+        s.h[4 * hi + 1] ^= s.h[4 * hi];
+      }
 #pragma unroll
-      for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi + 2, 4 * hi + 3, Tb);
+      for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi + 2, 4 * hi + 3, Tb);  // stage 8, p9 = 1 block
 #pragma unroll
       for (int hi = 0; hi < 4; ++hi) {
-        ib(s, 4 * hi, 4 * hi + 2, Ta);
-        ib(s, 4 * hi + 1, 4 * hi + 3, Ta);
+        s.l[4 * hi + 2] ^= s.l[4 * hi];  // stage 9
+        s.h[4 * hi + 2] ^= s.h[4 * hi];
       }
     }
 
     STAMP(4);
-    // ---- phase 3: formal derivative (poly_encoder.hpp:195-215), closed form,
-    // in place: register r only needs partners r | 2^b > r (still original when
-    // r is processed in increasing order) and other lanes' original register r
-    {
+    // ---- phases 3 + 4a: formal derivative (poly_encoder.hpp:195-215) and FFT
+    // stages 9, 8 (afft, additive_fft.hpp:121-141) for the outputs y < 256 only.
+    // Those FFT stages keep the block at j = d, whose skew skews[d - 1] is
+    // 0xFFFF: a ^= b * skew is a no-op, so they pass c'[y] through for y < 256,
+    // and the derivative is needed at y < 256 only.  Its closed form
+    // c'[y] = c[y] ^ XOR_{b: y_b = 0} c[y | 2^b] there reads
+    //   c'[y] = c0[y] ^ c1[y] ^ c2[y] ^ XOR_{b < 8, y_b = 0} c0[y | 2^b]
+    // with c0 / c1 / c2 = registers 4 q / 4 q + 1 / 4 q + 2 (p8 p9 = 00 / 10 /
+    // 01), q bit 0 = p6, bit 1 = p7, lane bits = p0..p5.
+    uint32_t ql[4], qh[4];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        uint32_t al = 0, ah = 0;
+    for (int q = 0; q < 4; ++q) {
+      uint32_t al = s.l[4 * q + 1] ^ s.l[4 * q + 2], ah = s.h[4 * q + 1] ^ s.h[4 * q + 2];
 #pragma unroll
-        for (int lb = 0; lb < 6; ++lb) {  // lane bits 0..5 = p0..p5
-          const uint32_t m = ((lane >> lb) & 1) ? 0u : 0xffffffffu;
-          al ^= from_upper(s.l[r], lb) & m;
-          ah ^= from_upper(s.h[r], lb) & m;
-        }
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb)  // r bit0 = p8, bit1 = p9, bit2 = p6, bit3 = p7
-          if (!(r & (1 << rb))) {
-            al ^= s.l[r | (1 << rb)];
-            ah ^= s.h[r | (1 << rb)];
-          }
-        s.l[r] ^= al;
-        s.h[r] ^= ah;
+      for (int lb = 0; lb < 6; ++lb) {  // lane bits 0..5 = p0..p5
+        const uint32_t m = ((lane >> lb) & 1) ? 0u : 0xffffffffu;
+        al ^= from_upper(s.l[4 * q], lb) & m;
+        ah ^= from_upper(s.h[4 * q], lb) & m;
       }
+      if (!(q & 1)) {  // p6 = 0
+        al ^= s.l[4 * (q | 1)];
+        ah ^= s.h[4 * (q | 1)];
+      }
+      if (!(q & 2)) {  // p7 = 0
+        al ^= s.l[4 * (q | 2)];
+        ah ^= s.h[4 * (q | 2)];
+      }
+      ql[q] = s.l[4 * q] ^ al;
+      qh[q] = s.h[4 * q] ^ ah;
     }
-
     STAMP(5);
-    // ---- phase 4: FFT_1024 restricted to outputs < 256 (afft, additive_fft.hpp:121-141)
-    uint32_t ql[4], qh[4];  // live registers: r with p8 = p9 = 0 -> q = (p6, p7)
-    {
-      Tab T, T8;
-      tab_at(tabs, tlin(skew_idx(0, 9)), T);  // stage 9: keep v < 512 (a-side only)
-      tab_at(tabs, tlin(skew_idx(0, 8)), T8);
-#pragma unroll
-      for (int hi = 0; hi < 4; ++hi) {
-        mul_acc(s.l[4 * hi + 2], s.h[4 * hi + 2], T, s.l[4 * hi], s.h[4 * hi]);
-        mul_acc(s.l[4 * hi + 3], s.h[4 * hi + 3], T, s.l[4 * hi + 1], s.h[4 * hi + 1]);
-      }
-      T = T8;  // stage 8: keep v < 256
-#pragma unroll
-      for (int hi = 0; hi < 4; ++hi) {
-        mul_acc(s.l[4 * hi + 1], s.h[4 * hi + 1], T, s.l[4 * hi], s.h[4 * hi]);
-        ql[hi] = s.l[4 * hi];
-        qh[hi] = s.h[4 * hi];
-      }
-    }
     STAMP(6);
     __syncthreads();  // every wave is done with its region: reuse them for E[y] tables
     if (!(DEC_ABL & 16))

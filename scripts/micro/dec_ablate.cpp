@@ -39,10 +39,10 @@ int main() {
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
-  for (int i = 0; i < 2; ++i) launch_reconstruct_n1024(p, t, sh, sl, ss, dp, de, B, out, sl * 256, nullptr);
+  for (int i = 0; i < 2; ++i) launch_reconstruct_n1024(p, t, sh, sl, ss, dp, de, nullptr, B, out, sl * 256, nullptr);
   (void)hipEventRecord(a);
   const int reps = 10;
-  for (int i = 0; i < reps; ++i) launch_reconstruct_n1024(p, t, sh, sl, ss, dp, de, B, out, sl * 256, nullptr);
+  for (int i = 0; i < reps; ++i) launch_reconstruct_n1024(p, t, sh, sl, ss, dp, de, nullptr, B, out, sl * 256, nullptr);
   (void)hipEventRecord(b);
   (void)hipEventSynchronize(b);
   float ms = 0;
