@@ -221,21 +221,30 @@ __device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t b
   }
 }
 
+__device__ __forceinline__ void bxor(State &s, int ra, int rb) {  // b ^= a (no multiply)
+#pragma unroll
+  for (int g = 0; g < GP; ++g) {
+    s.l[g][rb] ^= s.l[g][ra];
+    s.h[g][rb] ^= s.h[g][ra];
+  }
+}
+
 // layout C: register bit0 = p6, bit1 = p7, bit2 = p5 (passenger); stages 6, 7
-// have lane-uniform skews.
-__device__ __forceinline__ void ipassC(State &s, const uint8_t *tabs, uint32_t off) {
-  Tab Ta, Tb;
-  lds_tab_at(tabs, tlin(skew_idx(0, 6, off)), Ta);
-  lds_tab_at(tabs, tlin(skew_idx(1u << 7, 6, off)), Tb);
-  ibfly(s, 0, 1, Ta);
-  ibfly(s, 4, 5, Ta);
-  lds_tab_at(tabs, tlin(skew_idx(0, 7, off)), Ta);  // stage 7
-  ibfly(s, 2, 3, Tb);
+// have lane-uniform skews.  Only the IFFT at index 0 runs here, where the
+// block at j = d of a stage has skew skews[d - 1] = 0xFFFF (inverse_afft skips
+// the multiply): stage 7 (j = 128) and stage 6's first block (j = 64) are
+// b ^= a only.
+__device__ __forceinline__ void ipassC0(State &s, const uint8_t *tabs) {
+  Tab Tb;
+  lds_tab_at(tabs, tlin(skew_idx(1u << 7, 6, 0)), Tb);
+  bxor(s, 0, 1);  // stage 6, j = 64
+  bxor(s, 4, 5);
+  ibfly(s, 2, 3, Tb);  // stage 6, j = 192
   ibfly(s, 6, 7, Tb);
-  ibfly(s, 0, 2, Ta);
-  ibfly(s, 1, 3, Ta);
-  ibfly(s, 4, 6, Ta);
-  ibfly(s, 5, 7, Ta);
+  bxor(s, 0, 2);  // stage 7, j = 128
+  bxor(s, 1, 3);
+  bxor(s, 4, 6);
+  bxor(s, 5, 7);
 }
 
 __device__ __forceinline__ void fpassC(State &s, const uint8_t *tabs, uint32_t off) {
@@ -634,7 +643,7 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     exchange<LA, LB>(s, xch, xb, q, inst);
     ipass3(s, tabs, posB(q, 0), 3, 0);
     exchange<LB, LC>(s, xch, xb, q, inst);
-    ipassC(s, tabs, 0);
+    ipassC0(s, tabs);
     const State coef = s;
 
     // ---- FFT_256 at each coset shift (encodeLow, poly_encoder.hpp:229-237)
