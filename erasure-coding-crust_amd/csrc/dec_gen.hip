@@ -34,9 +34,13 @@ __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ?
 
 // inverse pass over register bits 0..NS-1 (position bits B0..) of
 // the local index pos & (n - 1); lb = tlin of the (masked) lane part
+// When the pass holds the top local bit (B0 + NS == L), the lane part of a
+// skew index has no bits above the stage, so a register block whose bits above
+// the stage are 0 (blk < 2d) has skew skews[d - 1] = 0xFFFF: b ^= a only.
 template <int B0, int NS, int L>
 __device__ __forceinline__ void ipassg(S16 &s, const uint8_t *tabs, uint32_t lb) {
   constexpr uint32_t NM = (1u << L) - 1;
+  constexpr bool TOP = B0 + NS == L;
   Tab T[2];
   tab_at(tabs, lb ^ tlin(skew_idx(0, B0)), T[0]);
   int k = 0;
@@ -49,29 +53,35 @@ __device__ __forceinline__ void ipassg(S16 &s, const uint8_t *tabs, uint32_t lb)
       if (nt < NS)
         tab_at(tabs, lb ^ tlin(skew_idx((uint32_t(nblk) << B0) & NM, B0 + nt)), T[(k + 1) & 1]);
 #pragma unroll
-      for (int i = 0; i < d; ++i) ib(s, blk + i, blk + i + d, T[k & 1]);
+      for (int i = 0; i < d; ++i) {
+        if (TOP && ((blk << B0) & NM) >> (B0 + t + 1) == 0) bx(s, blk + i, blk + i + d);
+        else ib(s, blk + i, blk + i + d, T[k & 1]);
+      }
     }
   }
 }
 
-// layout C, L = 9 or 10: stage 8 (pairs r bit 0, skew by p9 when local) and stage 9 (L = 10)
+// layout C, L = 9 or 10: stage 8 (pairs r bit 0, skew by p9 when local) and
+// stage 9 (L = 10).  The transform is at index 0, so a stage's block at j = d
+// has skew skews[d - 1] = 0xFFFF (no multiply): stage 9, and stage 8's block
+// with p9 = 0 (for L = 9 p9 is an instance bit: all of stage 8), are b ^= a.
 template <int L>
 __device__ __forceinline__ void ipassCg(S16 &s, const uint8_t *tabs) {
-  constexpr uint32_t NM = (1u << L) - 1;
-  Tab Ta, Tb;
-  tab_at(tabs, tlin(skew_idx(0, 8)), Ta);
-  tab_at(tabs, tlin(skew_idx((1u << 9) & NM, 8)), Tb);
 #pragma unroll
-  for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi, 4 * hi + 1, Ta);
-#pragma unroll
-  for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi + 2, 4 * hi + 3, Tb);
+  for (int hi = 0; hi < 4; ++hi) bx(s, 4 * hi, 4 * hi + 1);
   if constexpr (L == 10) {
-    tab_at(tabs, tlin(skew_idx(0, 9)), Ta);
+    Tab Tb;
+    tab_at(tabs, tlin(skew_idx(1u << 9, 8)), Tb);
+#pragma unroll
+    for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi + 2, 4 * hi + 3, Tb);
 #pragma unroll
     for (int hi = 0; hi < 4; ++hi) {
-      ib(s, 4 * hi, 4 * hi + 2, Ta);
-      ib(s, 4 * hi + 1, 4 * hi + 3, Ta);
+      bx(s, 4 * hi, 4 * hi + 2);
+      bx(s, 4 * hi + 1, 4 * hi + 3);
     }
+  } else {
+#pragma unroll
+    for (int hi = 0; hi < 4; ++hi) bx(s, 4 * hi + 2, 4 * hi + 3);
   }
 }
 
@@ -227,7 +237,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
     if constexpr (L <= 8) {
       ipassg<4, L - 4, L>(s, tabs, lbB());
       __builtin_amdgcn_sched_barrier(0);
-      derivative<LB, L>(s, lane);
+      derivative<LB, L, KB>(s, lane);
       __builtin_amdgcn_sched_barrier(0);
       fft_restricted<LB, L, KB>(s, tabs, lane);
     } else {
@@ -236,7 +246,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
       exchange<LB, LC>(s, my, lane);
       ipassCg<L>(s, tabs);
       __builtin_amdgcn_sched_barrier(0);
-      derivative<LC, L>(s, lane);
+      derivative<LC, L, KB>(s, lane);
       __builtin_amdgcn_sched_barrier(0);
       fft_restricted<LC, L, KB>(s, tabs, lane);
     }

@@ -202,7 +202,10 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   // present (and < nv), bits 0-15 = mul_index(E[v]).  Loaded one tile ahead so
   // the gather's table loads and the output-table fill wait on one global
   // latency instead of two (present/E, then the table).
-  auto load_meta = [&](uint64_t tl, uint32_t tid, uint32_t (&m)[2]) {
+  // m[2], m[3]: the output rows y = 4 lane + q (q = 0..3) of phase 5, 16 bits
+  // each: 0xFFFF = present (copied from the shard), else mul_index(E[y]) (the
+  // erased value is scaled by E[y]; y < 256 < nv always holds for n = 1024).
+  auto load_meta = [&](uint64_t tl, uint32_t tid, uint32_t (&m)[4]) {
     const uint64_t bb = tl / tiles_pp, pt = pattern ? pattern[bb] : bb;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -210,8 +213,18 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       const uint32_t p = present[pt * N + v], e = elog[pt * N + v];
       m[half] = mul_index(e) | ((p != 0 && int(v) < nv) ? 0x10000u : 0u);
     }
+    const uint32_t y0 = 4 * (tid & 63);
+    const uint32_t p4 = *reinterpret_cast<const uint32_t *>(present + pt * N + y0);
+    const uint2 e4 = *reinterpret_cast<const uint2 *>(elog + pt * N + y0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t e = ((q < 2 ? e4.x : e4.y) >> (16 * (q & 1))) & 0xFFFFu;
+      const uint32_t f = ((p4 >> (8 * q)) & 0xFFu) ? 0xFFFFu : mul_index(e);
+      if (q & 1) m[2 + (q >> 1)] |= f << 16;
+      else m[2 + (q >> 1)] = f;
+    }
   };
-  uint32_t meta[2] = {0, 0}, meta_next[2] = {0, 0};
+  uint32_t meta[4] = {0, 0, 0, 0}, meta_next[4] = {0, 0, 0, 0};
   if (blockIdx.x < total) load_meta(blockIdx.x, tid0, meta);
   for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
     // lane-derived addresses are recomputed per tile from an opaque copy of
@@ -222,10 +235,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     const uint32_t lane = tid & 63;
     const uint64_t b = tile / tiles_pp;
     const uint64_t col0 = (tile % tiles_pp) * COLS;
-    const uint64_t pt = pattern ? pattern[b] : b;  // erasure pattern of payload b
     const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
-    const uint8_t *pr = present + pt * N;
-    const uint16_t *E = elog + pt * N;
     uint8_t *O = out + b * ostride;
 
     // ---- phase 1: gather + scale rows v = tid, tid + 512 (decode_main:174-177)
@@ -279,6 +289,34 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     STAMP(2);
     __syncthreads();
     STAMP(3);
+    // phase-5 operands requested now, consumed after the transform (latency
+    // hidden behind it): the E[y] multiply tables of this lane's erased output
+    // rows y = 4 lane + q and the 8 bytes of its present ones
+    const uint64_t cbase = col0 + 4 * wave;
+    const bool whole = cbase + 4 <= ncols;
+    Tab T5[4];
+    uint32_t ra[4], rc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t y = 4 * lane + q;
+      const uint32_t m = (meta[2 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
+      ra[q] = rc[q] = 0;
+      if (m != 0xFFFFu) {
+        load_tab(t.mtab, m, T5[q]);
+      } else {
+        const uint8_t *row = SH + uint64_t(y) * sstride + 2 * cbase;
+        if (whole) {
+          const uint2 d = *reinterpret_cast<const uint2 *>(row);
+          ra[q] = d.x;
+          rc[q] = d.y;
+        } else {
+          for (uint64_t e = 0; e < 2 * (ncols > cbase ? ncols - cbase : 0); ++e) {
+            if (e < 4) ra[q] |= uint32_t(row[e]) << (8 * e);
+            else rc[q] |= uint32_t(row[e]) << (8 * (e - 4));
+          }
+        }
+      }
+    }
 
     // ---- phase 2: IFFT_1024 on this wave's group
     S16 s;
@@ -375,9 +413,6 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     }
     STAMP(5);
     STAMP(6);
-    __syncthreads();  // every wave is done with its region: reuse them for E[y] tables
-    if (!(DEC_ABL & 16))
-      OutTabs::fill(regions, t.mtab, K, [&](uint32_t y) { return mul_index(E[y]); }, tid, THREADS);
     STAMP(7);
     {
       // q bit0 = p6, bit1 = p7; lane bits = p0..p5.  Positions < 256 only.
@@ -469,37 +504,22 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       fb(2, 3, T[1]);
     }
     STAMP(8);
-    __syncthreads();  // E[y] tables in place
     STAMP(9);
 
     // ---- phase 5: y = 4*lane + q; columns col0 + 4*wave + c (decode_main:185-188,
-    // reconstructSub:138-149)
+    // reconstructSub:138-149).  No workgroup barrier: the operands were
+    // requested before the transform.
     {
-      const uint64_t cbase = col0 + 4 * wave;
       uint32_t ol[4], oh[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const uint32_t y = 4 * lane + q;
+        const uint32_t m = (meta[2 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
         ol[q] = oh[q] = 0;
-        if (!(DEC_ABL & 8) && int(y) < nv && pr[y]) {
-          const uint8_t *row = SH + uint64_t(y) * sstride + 2 * cbase;
-          uint32_t a = 0, c = 0;
-          if (cbase + 4 <= ncols) {
-            const uint2 d = *reinterpret_cast<const uint2 *>(row);
-            a = d.x;
-            c = d.y;
-          } else {
-            for (uint64_t e = 0; e < 2 * (ncols > cbase ? ncols - cbase : 0); ++e) {
-              if (e < 4) a |= uint32_t(row[e]) << (8 * e);
-              else c |= uint32_t(row[e]) << (8 * (e - 4));
-            }
-          }
-          oh[q] = vperm(c, a, 0x06040200u);
-          ol[q] = vperm(c, a, 0x07050301u);
+        if (m != 0xFFFFu) {
+          mul_acc(ql[q], qh[q], T5[q], ol[q], oh[q]);
         } else {
-          Tab T;
-          OutTabs::load(regions, y, T);
-          mul_acc(ql[q], qh[q], T, ol[q], oh[q]);
+          oh[q] = vperm(rc[q], ra[q], 0x06040200u);
+          ol[q] = vperm(rc[q], ra[q], 0x07050301u);
         }
       }
       // column c of the group: 4 consecutive y -> 8 bytes BE
@@ -516,8 +536,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       }
     }
     STAMP(10);
-    meta[0] = meta_next[0];
-    meta[1] = meta_next[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) meta[i] = meta_next[i];
   }
 #ifdef DEC_STAMP
   if ((threadIdx.x & 63) == 0)

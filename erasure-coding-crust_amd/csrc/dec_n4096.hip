@@ -189,17 +189,44 @@ reconstruct_n4096(
         Qq.l[r] = x.x;
         Qq.h[r] = x.y;
       }
-      ifft1024(Qq, tabs, my, lq);  // -> layout C
+      if (q == 0) ifft1024<true>(Qq, tabs, my, lq);  // -> layout C; quarter 0 is at index 0
+      else ifft1024<false>(Qq, tabs, my, lq);
       __builtin_amdgcn_sched_barrier(0);
-      Tab TP, TK;
+      // P += p_q u_q, Qa += k_q u_q.  The constants are mostly 0 or 1 (the
+      // skews at 1023 and 2047 are 0xFFFF: n = 4096 gives p = (1, 0, 0, 0),
+      // k = (0, 1, 1 + s, s); n = 2048 p = (1, 0), k = (1, 1)), so each is a
+      // uniform branch: skip (log 65535 = zero), XOR (log 0 = one) or multiply.
+      // Qa is read at the registers reaching y < k only; P also at their
+      // single-bit partners (the derivative): everywhere but r & 3 == 3
+      // (p8 = p9 = 1) when k = 256.
       uint32_t ip = lin.p[q], ik = lin.k[q];
       asm volatile("" : "+s"(ip), "+s"(ik));  // loaded here, not hoisted (and kept live) from the top
-      load_tab(t.mtab, ip, TP);
-      load_tab(t.mtab, ik, TK);
+      if (ip == 0) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        mul_acc(Qq.l[r], Qq.h[r], TP, P.l[r], P.h[r]);
-        mul_acc(Qq.l[r], Qq.h[r], TK, Qa.l[r], Qa.h[r]);  // shares the selectors of the line above
+        for (int r = 0; r < 16; ++r) {
+          P.l[r] ^= Qq.l[r];
+          P.h[r] ^= Qq.h[r];
+        }
+      } else if (ip != 65535u) {
+        Tab TP;
+        load_tab(t.mtab, ip, TP);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (KB >= 9 || (r & 3) != 3) mul_acc(Qq.l[r], Qq.h[r], TP, P.l[r], P.h[r]);
+      }
+      if (ik == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (live_above<LC, 10, KB>(r, KB - 1)) {
+            Qa.l[r] ^= Qq.l[r];
+            Qa.h[r] ^= Qq.h[r];
+          }
+      } else if (ik != 65535u) {
+        Tab TK;
+        load_tab(t.mtab, ik, TK);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (live_above<LC, 10, KB>(r, KB - 1)) mul_acc(Qq.l[r], Qq.h[r], TK, Qa.l[r], Qa.h[r]);
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r)  // accumulated here, not sunk into the next quarter's gather
@@ -226,7 +253,7 @@ reconstruct_n4096(
     // k_q folded on the host from skews 1023 / 2047 / 3071: n4096_lin()).
     // D in closed form (poly_encoder.hpp:195-215) over bits 0..9, in place:
     // lane = p0..p5, r = (p8, p9, p6, p7).
-    derivative<LC, 10>(P, lane);
+    derivative<LC, 10, KB>(P, lane);  // at the registers reaching y < k only
     S16 Y;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -237,7 +264,7 @@ reconstruct_n4096(
     // ---- FFT_1024, index 0 (quarter 0's tables still resident): whole for
     // k = 1024 (-> layout A: y = 16 lane + r), else restricted to y < k
     // (tf1024.hpp fft_restricted: live register pairs hold y0, y0 + 1)
-    if constexpr (KB == 10) fft1024(Y, tabs, my, lane);
+    if constexpr (KB == 10) fft1024<true>(Y, tabs, my, lane);
     else fft_restricted<LC, 10, KB>(Y, tabs, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(Y.l[r]), "+v"(Y.h[r]));  // not sunk past the table gather

@@ -159,8 +159,8 @@ __global__ void __launch_bounds__(THREADS)
         store_half(regions, SH, sstride, 512 * hf, nv, piece0, npieces, wave, lane);
       }
       lds_barrier();
-      ifft1024(g0, tabs, my, lane);
-      ifft1024(g1, tabs, my, lane);
+      ifft1024<true>(g0, tabs, my, lane);  // index 0 (zero skews at the top stages)
+      ifft1024<true>(g1, tabs, my, lane);
       uint2 *c0 = coef_at(coef, tile, wave, 0), *c1 = coef_at(coef, tile, wave, 1);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {

@@ -136,6 +136,43 @@ __device__ __forceinline__ void fpassC(S16 &s, const uint8_t *tabs) {
   for (int hi = 0; hi < 4; ++hi) fb(s, 4 * hi + 2, 4 * hi + 3, Ta);
 }
 
+// The same two passes for the transform at index 0, where a stage's block at
+// j = d has skew skews[d - 1] = 0xFFFF (no multiply, additive_fft.hpp:99-141):
+// stage 9 and stage 8's p9 = 0 block are b ^= a (IFFT) / b ^= a after an
+// a ^= 0 (FFT).
+__device__ __forceinline__ void bx(S16 &s, int a, int b) {  // b ^= a
+  s.l[b] ^= s.l[a];
+  s.h[b] ^= s.h[a];
+}
+
+__device__ __forceinline__ void ipassC0(S16 &s, const uint8_t *tabs) {
+  Tab Tb;
+  tab_at(tabs, tlin(skew_idx(1u << 9, 8)), Tb);
+#pragma unroll
+  for (int hi = 0; hi < 4; ++hi) bx(s, 4 * hi, 4 * hi + 1);
+#pragma unroll
+  for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi + 2, 4 * hi + 3, Tb);
+#pragma unroll
+  for (int hi = 0; hi < 4; ++hi) {
+    bx(s, 4 * hi, 4 * hi + 2);
+    bx(s, 4 * hi + 1, 4 * hi + 3);
+  }
+}
+
+__device__ __forceinline__ void fpassC0(S16 &s, const uint8_t *tabs) {
+  Tab Ta;
+  tab_at(tabs, tlin(skew_idx(1u << 9, 8)), Ta);
+#pragma unroll
+  for (int hi = 0; hi < 4; ++hi) {
+    bx(s, 4 * hi, 4 * hi + 2);
+    bx(s, 4 * hi + 1, 4 * hi + 3);
+  }
+#pragma unroll
+  for (int hi = 0; hi < 4; ++hi) bx(s, 4 * hi, 4 * hi + 1);
+#pragma unroll
+  for (int hi = 0; hi < 4; ++hi) fb(s, 4 * hi + 2, 4 * hi + 3, Ta);
+}
+
 __device__ __forceinline__ uint32_t posA(uint32_t lane, int r) { return 16 * lane + uint32_t(r); }
 __device__ __forceinline__ uint32_t posB(uint32_t lane, int r) {
   return (lane & 15) | (uint32_t(r) << 4) | ((lane >> 4) << 8);
@@ -172,20 +209,25 @@ __device__ __forceinline__ void exchange(S16 &s, uint8_t *my, uint32_t lane) {
   __builtin_amdgcn_wave_barrier();
 }
 
-// IFFT_1024 (inverse_afft, index = the tables' offset): layout A in, C out
+// IFFT_1024 (inverse_afft, index = the tables' offset; INDEX0: the offset is
+// 0): layout A in, C out
+template <bool INDEX0 = false>
 __device__ __forceinline__ void ifft1024(S16 &s, const uint8_t *tabs, uint8_t *my, uint32_t lane) {
   asm volatile("" : "+v"(lane));
   ipass4<0>(s, tabs, tlin(16 * lane));
   exchange<LA, LB>(s, my, lane);
   ipass4<4>(s, tabs, tlin((lane >> 4) << 8));
   exchange<LB, LC>(s, my, lane);
-  ipassC(s, tabs);
+  if constexpr (INDEX0) ipassC0(s, tabs);
+  else ipassC(s, tabs);
 }
 
 // FFT_1024 (afft): layout C in, A out
+template <bool INDEX0 = false>
 __device__ __forceinline__ void fft1024(S16 &s, const uint8_t *tabs, uint8_t *my, uint32_t lane) {
   asm volatile("" : "+v"(lane));
-  fpassC(s, tabs);
+  if constexpr (INDEX0) fpassC0(s, tabs);
+  else fpassC(s, tabs);
   exchange<LC, LB>(s, my, lane);
   fpass4<4>(s, tabs, tlin((lane >> 4) << 8));
   exchange<LB, LA>(s, my, lane);
@@ -231,11 +273,22 @@ __host__ __device__ constexpr int lane_pbit(int u) {
 
 // formal derivative (poly_encoder.hpp:195-215), closed form, in layout X, in
 // place: registers in increasing order (register partners r | 2^t > r are
-// still original), lane partners read the other lanes' original register r
-template <Layout X, int L>
+// still original), lane partners read the other lanes' original register r.
+// Only registers with LIVE(r) are computed (the others keep their values, so
+// they still read as original partners): before fft_restricted<X, L, KB> the
+// registers that reach y < k, since its stages t >= KB pass y < k through.
+template <Layout X, int L, int KB = L>
+__device__ __forceinline__ void derivative(S16 &s, uint32_t lane);
+
+// register r is still needed after the a-only stages above t (t = KB - 1: all)
+template <Layout X, int L, int KB>
+__host__ __device__ constexpr bool live_above(int r, int t);
+
+template <Layout X, int L, int KB>
 __device__ __forceinline__ void derivative(S16 &s, uint32_t lane) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
+    if (!live_above<X, L, KB>(r, KB - 1)) continue;
     uint32_t al = 0, ah = 0;
 #pragma unroll
     for (int u = 0; u < 6; ++u) {
@@ -256,10 +309,11 @@ __device__ __forceinline__ void derivative(S16 &s, uint32_t lane) {
 }
 
 
-// ---- FFT_n restricted to the outputs y < k = 2^KB (afft, additive_fft.hpp:121-141),
-// from the layout the derivative ran in (X = C for n >= 512, B below):
-//  * register-held stages t >= KB keep only the side that reaches y < k
-//    (a ^= b * s); registers with such a bit set are dead afterwards;
+// ---- FFT_n restricted to the outputs y < k = 2^KB (afft, additive_fft.hpp:121-141,
+// index 0), from the layout the derivative ran in (X = C for n >= 512, B below):
+//  * register-held stages t >= KB: only the side that reaches y < k is kept
+//    (a ^= b * s), and that is the block at j = 2^t whose skew skews[2^t - 1]
+//    is 0xFFFF (no multiply): these stages pass y < k through, nothing runs;
 //  * register-held stages below KB are full butterflies on the live registers;
 //  * the lane-held stages (p5..p0 in C, p3..p0 in B) run in registers after
 //    swapping each lane bit with register bit SB (the one of p6 / p4, whose
@@ -270,7 +324,6 @@ __host__ __device__ constexpr int rbit_of(int p) {
   return reg_pbit<X>(0) == p ? 0 : reg_pbit<X>(1) == p ? 1 : reg_pbit<X>(2) == p ? 2
                                  : reg_pbit<X>(3) == p ? 3 : -1;
 }
-// register r is still needed after the a-only stages above t (t = KB - 1: all)
 template <Layout X, int L, int KB>
 __host__ __device__ constexpr bool live_above(int r, int t) {
   for (int p = (t + 1 > KB ? t + 1 : KB); p < L; ++p) {
@@ -329,15 +382,14 @@ __device__ __forceinline__ void fft_restricted(S16 &s, const uint8_t *tabs, uint
   constexpr int SB = swap_rbit<X>(), NL = lane_stages<X>();
   // register-held stages L-1 .. F (tables: wave-uniform, from the register bits above t)
 #pragma unroll
-  for (int t = L - 1; t >= F; --t) {
+  for (int t = (KB - 1 < L - 1 ? KB - 1 : L - 1); t >= F; --t) {
     const int b = rbit_of<X>(t);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       if (((r >> b) & 1) || !live_above<X, L, KB>(r, t)) continue;
       Tab T;
       tab_at(tabs, tlin(skew_idx(reg_pos<X, L>(r, -1), t)), T);
-      if (t >= KB) mul_acc(s.l[r | (1 << b)], s.h[r | (1 << b)], T, s.l[r], s.h[r]);  // a-side only
-      else fb(s, r, r | (1 << b), T);
+      fb(s, r, r | (1 << b), T);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
