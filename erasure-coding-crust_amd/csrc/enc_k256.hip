@@ -2,17 +2,19 @@
 // (n_validators 766..1024, the BASELINE headline configuration).
 //
 // Work decomposition:
-//  * persistent: one 512-thread workgroup per CU, looping over tiles of 128
-//    consecutive pieces (piece = 512 payload bytes = 256 GF(2^16) symbols);
-//  * wave w owns pieces [16w, 16w+16) of the tile: 2 "instances" (lanes
-//    0-31 / 32-63) x 2 byte-planar groups (registers) x 4 pieces;
+//  * persistent: one 1024-thread workgroup (16 waves, 4 per SIMD) per CU,
+//    looping over tiles of 128 consecutive pieces (piece = 512 payload bytes
+//    = 256 GF(2^16) symbols);
+//  * wave w owns pieces [8w, 8w+8) of the tile: 2 "instances" (lanes 0-31 /
+//    32-63) x 1 byte-planar group (registers) x 4 pieces;
 //  * within an instance, lane q holds 8 of the 256 positions in registers:
 //    every radix-8 pass runs 3 butterfly stages in registers, then the wave
 //    re-distributes positions through its private LDS region;
 //  * multiplies: v_perm tables (ec_device.hpp) for every skew the k=256 /
 //    n=1024 code uses (1023 x 80 B) are resident in LDS for the whole kernel;
-//  * shard stores: results are staged in LDS as [shard row][128 pieces] and
-//    written as 256-byte contiguous row segments (two rows per wave store).
+//  * shard stores: each wave stages its 8 pieces x 256 rows in its own LDS
+//    region; all waves then write 256-byte contiguous row segments
+//    (global_store_dwordx4, 16 B per lane).
 // Butterflies, skew indices and the encodeLow structure follow
 // include/ec-cpp/additive_fft.hpp:99-141 and poly_encoder.hpp:217-240.
 #include <hip/hip_runtime.h>
@@ -20,43 +22,13 @@
 #include "ec_device.hpp"
 #include "ec_kernels.hpp"
 
-// ENC_ABL: ablation switches for scripts/micro/enc_ablate.cpp only (results are
-// wrong when set): 1 = no shard stores, 2 = one table load per pass,
-// 4 = no exchanges, 8 = no staging/stores at all, 16 = staging reads kept but
-// no global stores.
-#ifndef ENC_ABL
-#define ENC_ABL 0
-#endif
-
 namespace ecamd {
 namespace {
 
 constexpr int K = 256;
-// GP byte-planar groups per lane (registers), WAVES per workgroup.  GP = 1 with
-// 16 waves gives 4 waves/SIMD (<= 128 VGPRs) for latency hiding; the tile is
-// 128 pieces either way.
-#ifndef ENC_GP
-#define ENC_GP 1
-#endif
-constexpr int GP = ENC_GP;
-#ifndef ENC_DIRECT
-#define ENC_DIRECT 0
-#endif
-constexpr bool kDirect = ENC_DIRECT;
-#ifndef ENC_OWN
-#define ENC_OWN 1
-#endif
-constexpr bool kOwn = ENC_OWN;
-#ifndef ENC_WIDE
-#define ENC_WIDE 1
-#endif
-#if ENC_WIDE
-#define STAGE stage_rows16
-#define STORE store_rows16
-#else
-#define STAGE stage_rows
-#define STORE store_rows
-#endif
+// one byte-planar group per lane (GP = 1) and 16 waves: 4 waves/SIMD (<= 128
+// VGPRs) for latency hiding; the tile is 128 pieces
+constexpr int GP = 1;
 constexpr int WAVES = 16 / GP;
 constexpr int THREADS = 64 * WAVES;
 constexpr int TILE = 8 * GP * WAVES;  // pieces per tile
@@ -70,13 +42,6 @@ static_assert(TILE == 128 && 256 * 256 <= WAVES * XCH_BYTES, "staging fits the e
 struct State {
   uint32_t l[GP][8], h[GP][8];  // [group][register]: low / high byte planes
 };
-
-__device__ __forceinline__ void lds_tab(const uint8_t *lds, uint32_t idx, Tab &T,
-                                        bool &first) {
-  if ((ENC_ABL & 2) && !first) return;
-  first = false;
-  Tabs::load(lds, idx, T);
-}
 
 // GF(2)-linear part of the swizzled table address (LdsTabs::addr without the
 // plane term): tlin(a | b) = tlin(a) ^ tlin(b) for disjoint a, b.  A table index
@@ -124,16 +89,11 @@ __device__ __forceinline__ void fbfly(State &s, int ra, int rb, const Tab &T) {
 // Table loads are software-pipelined: the next butterfly group's table is
 // requested before the current group's multiplies, so a wave keeps one 80-B
 // table load in flight instead of stalling on each (2 x 20 VGPRs).
-#ifndef ENC_PIPE
-#define ENC_PIPE 1
-#endif
-
 // radix-8 pass over 3 consecutive position bits b0..b0+2 held in registers:
 // pos(r) = base | (r << b0).  Inverse: stages b0, b0+1, b0+2.
 __device__ __forceinline__ void ipass3(State &s, const uint8_t *tabs, uint32_t base, int b0,
                                        uint32_t off) {
-  bool first = true;
-  if constexpr (ENC_PIPE) {
+  {
     Tab Ta, Tb;
     const uint32_t lb = tlin(base & ~((2u << b0) - 1));  // lane part of every index below
     const auto i0 = [&](int rr) { return lb ^ tlin(skew_idx(uint32_t(2 * rr) << b0, b0, off)); };
@@ -156,30 +116,13 @@ __device__ __forceinline__ void ipass3(State &s, const uint8_t *tabs, uint32_t b
     ibfly(s, 5, 7, Tb);
 #pragma unroll
     for (int r = 0; r < 4; ++r) ibfly(s, r, r + 4, Ta);
-    return;
   }
-  Tab T;
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {  // stage b0: 4 distinct skews
-    lds_tab(tabs, skew_idx(base | (uint32_t(2 * rr) << b0), b0, off), T, first);
-    ibfly(s, 2 * rr, 2 * rr + 1, T);
-  }
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {  // stage b0+1: 2 distinct skews
-    lds_tab(tabs, skew_idx(base | (uint32_t(4 * hh) << b0), b0 + 1, off), T, first);
-    ibfly(s, 4 * hh, 4 * hh + 2, T);
-    ibfly(s, 4 * hh + 1, 4 * hh + 3, T);
-  }
-  lds_tab(tabs, skew_idx(base, b0 + 2, off), T, first);  // stage b0+2: 1 skew
-#pragma unroll
-  for (int r = 0; r < 4; ++r) ibfly(s, r, r + 4, T);
 }
 
 // forward: stages b0+2, b0+1, b0
 __device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t base, int b0,
                                        uint32_t off) {
-  bool first = true;
-  if constexpr (ENC_PIPE) {
+  {
     Tab Ta, Tb;
     const uint32_t lb = tlin(base & ~((2u << b0) - 1));  // lane part of every index below
     const auto i0 = [&](int rr) { return lb ^ tlin(skew_idx(uint32_t(2 * rr) << b0, b0, off)); };
@@ -202,22 +145,6 @@ __device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t b
     lds_tab_at(tabs, i0(3), Ta);
     fbfly(s, 4, 5, Tb);
     fbfly(s, 6, 7, Ta);
-    return;
-  }
-  Tab T;
-  lds_tab(tabs, skew_idx(base, b0 + 2, off), T, first);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) fbfly(s, r, r + 4, T);
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
-    lds_tab(tabs, skew_idx(base | (uint32_t(4 * hh) << b0), b0 + 1, off), T, first);
-    fbfly(s, 4 * hh, 4 * hh + 2, T);
-    fbfly(s, 4 * hh + 1, 4 * hh + 3, T);
-  }
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    lds_tab(tabs, skew_idx(base | (uint32_t(2 * rr) << b0), b0, off), T, first);
-    fbfly(s, 2 * rr, 2 * rr + 1, T);
   }
 }
 
@@ -267,19 +194,8 @@ __device__ __forceinline__ uint32_t posA(uint32_t q, int r) { return (q << 3) | 
 __device__ __forceinline__ uint32_t posB(uint32_t q, int r) {
   return ((q >> 3) << 6) | (uint32_t(r) << 3) | (q & 7);
 }
-[[maybe_unused]] __device__ __forceinline__ uint32_t posC(uint32_t q, int r) {
-  return (uint32_t(r & 3) << 6) | (uint32_t(r >> 2) << 5) | q;
-}
-
 // ---- wave-private exchange -------------------------------------------------
-// GP = 2: 16-byte cell (pos, inst) = both groups; 256-byte windows of 8 positions
-// with the cell XOR-swizzled by h(window) (layout A/B/C reads conflict-free).
-[[maybe_unused]] __device__ __forceinline__ uint32_t xaddr16(uint32_t pos, uint32_t inst) {
-  const uint32_t w = pos >> 3;
-  const uint32_t h = (w & 15) ^ ((w >> 3) & 1);
-  return (w << 8) | ((((pos & 7) * 2 + inst) ^ h) << 4);
-}
-// GP = 1: 8-byte cell u = pos*2 + inst mapped by a GF(2)-linear bijection M
+// 8-byte cell u = pos*2 + inst mapped by a GF(2)-linear bijection M
 // (found by search, scripts/search_swizzle.py) under which every layout's
 // reads (32-lane groups) and writes (16-lane groups) are bank-conflict free.
 // u = lane part XOR register part, so addr = M(lane part) ^ M(r part).
@@ -304,59 +220,32 @@ __host__ __device__ constexpr uint32_t uregC(int r) {
 
 enum Layout { LA, LB, LC };
 
-struct XBase {  // per-lane exchange base addresses (GP = 1)
+struct XBase {  // per-lane exchange base addresses
   uint32_t a, b, c;
 };
 
 template <Layout L>
-__device__ __forceinline__ uint32_t xcell(const XBase &xb, uint32_t q, uint32_t inst, int r) {
-  if constexpr (GP == 1) {
-    if constexpr (L == LA) return xb.a ^ mswz(uregA(r));
-    else if constexpr (L == LB) return xb.b ^ mswz(uregB(r));
-    else return xb.c ^ mswz(uregC(r));
-  } else {
-    const uint32_t pos = L == LA ? posA(q, r) : (L == LB ? posB(q, r) : posC(q, r));
-    return xaddr16(pos, inst);
-  }
+__device__ __forceinline__ uint32_t xcell(const XBase &xb, int r) {
+  if constexpr (L == LA) return xb.a ^ mswz(uregA(r));
+  else if constexpr (L == LB) return xb.b ^ mswz(uregB(r));
+  else return xb.c ^ mswz(uregC(r));
 }
 
 template <Layout FROM, Layout TO>
-__device__ __forceinline__ void exchange(State &s, uint8_t *xch, const XBase &xb, uint32_t q,
-                                         uint32_t inst) {
-  if (ENC_ABL & 4) return;
+__device__ __forceinline__ void exchange(State &s, uint8_t *xch, const XBase &xb) {
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    if constexpr (GP == 1)
-      *reinterpret_cast<uint2 *>(xch + xcell<FROM>(xb, q, inst, r)) =
-          make_uint2(s.l[0][r], s.h[0][r]);
-    else
-      *reinterpret_cast<uint4 *>(xch + xcell<FROM>(xb, q, inst, r)) =
-          make_uint4(s.l[0][r], s.h[0][r], s.l[GP - 1][r], s.h[GP - 1][r]);
-  }
+  for (int r = 0; r < 8; ++r)
+    *reinterpret_cast<uint2 *>(xch + xcell<FROM>(xb, r)) = make_uint2(s.l[0][r], s.h[0][r]);
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
-    if constexpr (GP == 1) {
-      const uint2 v = *reinterpret_cast<const uint2 *>(xch + xcell<TO>(xb, q, inst, r));
-      s.l[0][r] = v.x;
-      s.h[0][r] = v.y;
-    } else {
-      const uint4 v = *reinterpret_cast<const uint4 *>(xch + xcell<TO>(xb, q, inst, r));
-      s.l[0][r] = v.x;
-      s.h[0][r] = v.y;
-      s.l[GP - 1][r] = v.z;
-      s.h[GP - 1][r] = v.w;
-    }
+    const uint2 v = *reinterpret_cast<const uint2 *>(xch + xcell<TO>(xb, r));
+    s.l[0][r] = v.x;
+    s.h[0][r] = v.y;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
-}
-
-// staging row v (shard offset), 128 pieces x 2 bytes; 8-byte slots XOR-swizzled
-// by the row's position block so the layout-A writes and row reads are conflict free
-__device__ __forceinline__ uint32_t saddr(uint32_t v, uint32_t slot8) {
-  return v * 256 + ((slot8 ^ ((v >> 3) & 31)) << 3);
 }
 
 // byte-planar group (4 pieces) -> big-endian u16 x4 (pieces 0..3 in order)
@@ -364,93 +253,7 @@ __device__ __forceinline__ uint2 to_be(uint32_t l, uint32_t h) {
   return make_uint2(vperm(l, h, 0x05010400u), vperm(l, h, 0x07030602u));
 }
 
-// registers in layout A -> LDS staging rows 0..255 (shard = s0 + row)
-[[maybe_unused]] __device__ __forceinline__ void stage_rows(const State &s, uint8_t *stg, uint32_t q, uint32_t inst,
-                                           uint32_t wave) {
-  if (ENC_ABL & 8) return;
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const uint32_t v = posA(q, r);
-#pragma unroll
-    for (int g = 0; g < GP; ++g)  // pieces 8P*wave + 4P*inst + 4g .. +3
-      *reinterpret_cast<uint2 *>(stg + saddr(v, (2 * GP * wave + GP * inst + g))) =
-          to_be(s.l[g][r], s.h[g][r]);
-  }
-}
-
-// all waves: LDS rows -> shards [s0, s0+256), 256-byte row segments
-[[maybe_unused]] __device__ __forceinline__ void store_rows(const uint8_t *stg, uint8_t *SH, uint64_t sstride,
-                                           uint32_t s0, int nv, uint64_t piece0, uint64_t npieces,
-                                           uint32_t wave, uint32_t lane) {
-  if (ENC_ABL & 9) return;
-  const uint32_t c = lane & 31;  // 4 pieces per lane
-  const uint64_t p = piece0 + 4 * c;
-#pragma unroll 4
-  for (int it = 0; it < 128 / WAVES; ++it) {
-    const uint32_t v = uint32_t(it) * 2 * WAVES + wave * 2 + (lane >> 5);
-    const uint2 val = *reinterpret_cast<const uint2 *>(stg + saddr(v, c));
-    const uint32_t shard = s0 + v;
-    if (int(shard) >= nv) continue;
-    uint8_t *dst = SH + uint64_t(shard) * sstride + 2 * p;
-    if (ENC_ABL & 16) {  // ablation: LDS reads kept, global store skipped
-      if (val.x == 0x12345678u && val.y == 0x9abcdef0u) *dst = 1;
-    } else if (p + 4 <= npieces) {
-      *reinterpret_cast<uint2 *>(dst) = val;
-    } else if (p < npieces) {
-      const uint32_t w[2] = {val.x, val.y};
-      for (uint64_t e = 0; e < npieces - p; ++e)
-        *reinterpret_cast<uint16_t *>(dst + 2 * e) = uint16_t(w[e >> 1] >> (16 * (e & 1)));
-    }
-  }
-}
-
-// ---- 16-byte staging (GP = 1): row v = 16 slots of 16 B, slot w = pieces
-// [8w, 8w + 8) of the tile (wave w), half = inst; slots XOR-swizzled by
-// (v >> 3) & 15 so the 16-lane row reads are conflict free (the layout-A
-// writes are 2-way, 8 instructions per shift).
-__device__ __forceinline__ uint32_t saddr16(uint32_t v, uint32_t slot16) {
-  return v * 256 + ((slot16 ^ ((v >> 3) & 15)) << 4);
-}
-
-[[maybe_unused]] __device__ __forceinline__ void stage_rows16(const State &s, uint8_t *stg, uint32_t q,
-                                             uint32_t inst, uint32_t wave) {
-#pragma unroll
-  for (int r = 0; r < 8; ++r)
-    *reinterpret_cast<uint2 *>(stg + saddr16(posA(q, r), wave) + 8 * inst) =
-        to_be(s.l[0][r], s.h[0][r]);
-}
-
-// all waves: LDS rows -> shards [s0, s0 + 256); lane = (row-in-4, 16-B chunk),
-// one dwordx4 per lane per row: 4 store instructions per wave per shift.
-[[maybe_unused]] __device__ __forceinline__ void store_rows16(const uint8_t *stg, uint8_t *SH, uint64_t sstride,
-                                             uint32_t s0, int nv, uint64_t piece0,
-                                             uint64_t npieces, uint32_t wave, uint32_t lane) {
-  const uint32_t c = lane & 15;
-  const uint64_t p = piece0 + 8 * c;
-  const bool wide = ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0;  // 16-B aligned rows
-#pragma unroll
-  for (int it = 0; it < 256 / (4 * WAVES); ++it) {
-    const uint32_t v = uint32_t(it) * 4 * WAVES + wave * 4 + (lane >> 4);
-    const uint4 val = *reinterpret_cast<const uint4 *>(stg + saddr16(v, c));
-    const uint32_t shard = s0 + v;
-    if (int(shard) >= nv) continue;
-    uint8_t *dst = SH + uint64_t(shard) * sstride + 2 * p;
-    if (p + 8 <= npieces) {
-      if (wide) {
-        *reinterpret_cast<uint4 *>(dst) = val;
-      } else {
-        reinterpret_cast<uint2 *>(dst)[0] = make_uint2(val.x, val.y);
-        reinterpret_cast<uint2 *>(dst)[1] = make_uint2(val.z, val.w);
-      }
-    } else if (p < npieces) {
-      const uint32_t w[4] = {val.x, val.y, val.z, val.w};
-      for (uint64_t e = 0; e < npieces - p; ++e)
-        *reinterpret_cast<uint16_t *>(dst + 2 * e) = uint16_t(w[e >> 1] >> (16 * (e & 1)));
-    }
-  }
-}
-
-// ---- own-region staging (GP = 1): wave w stages its 8 pieces x 256 rows in
+// ---- own-region staging: wave w stages its 8 pieces x 256 rows in
 // its own 4 KB exchange region, 16 B per row (half = inst).  Row v sits in
 // 256-byte block v >> 4 at 16-B slot (v ^ (v >> 4) ^ w) & 15: the 16 lanes that
 // read one row from the 16 regions hit 16 distinct slots (conflict free) and
@@ -500,40 +303,6 @@ __device__ __forceinline__ void store_own(const uint8_t *xbase, uint8_t *SH, uin
   }
 }
 
-// registers in layout A -> shards [s0 + 8q, s0 + 8q + 8) straight from the
-// registers: lanes (q, 0) and (q, 1) write 16 contiguous bytes of a row; the
-// L2 merges the 16 waves' pieces into full lines.  No staging, no barriers.
-[[maybe_unused]] __device__ __forceinline__ void store_direct(const State &s, uint8_t *SH, uint64_t sstride,
-                                             uint32_t s0, int nv, uint64_t piece0,
-                                             uint64_t npieces, uint32_t q, uint32_t inst,
-                                             uint32_t wave) {
-  const uint64_t p = piece0 + 8 * GP * wave + 4 * GP * inst;
-  const uint32_t row0 = s0 + 8 * q;
-  uint8_t *dst = SH + uint64_t(row0) * sstride + 2 * p;
-  const bool full = p + 4 * GP <= npieces && int(row0 + 8) <= nv;
-  if (full) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-#pragma unroll
-      for (int g = 0; g < GP; ++g)
-        *reinterpret_cast<uint2 *>(dst + 8 * g) = to_be(s.l[g][r], s.h[g][r]);
-      dst += sstride;
-    }
-    return;
-  }
-  for (int r = 0; r < 8; ++r, dst += sstride) {
-    if (int(row0) + r >= nv) break;
-#pragma unroll
-    for (int g = 0; g < GP; ++g) {
-      const uint2 val = to_be(s.l[g][r], s.h[g][r]);
-      const uint64_t pg = p + 4 * g;
-      const uint32_t w[2] = {val.x, val.y};
-      for (uint64_t e = 0; pg + e < npieces && e < 4; ++e)
-        *reinterpret_cast<uint16_t *>(dst + 8 * g + 2 * e) = uint16_t(w[e >> 1] >> (16 * (e & 1)));
-    }
-  }
-}
-
 }  // namespace
 
 // N = n: 1024 (n_validators 766..1024) or 2048 (1025..1533); the cosets at
@@ -573,11 +342,9 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     const uint32_t inst = lane >> 5, q = lane & 31;
     uint8_t *xch = lds + TAB_REGION + wave * XCH_BYTES;
     XBase xb;
-    if constexpr (GP == 1) {
-      xb.a = mswz(ulaneA(q, inst));
-      xb.b = mswz(ulaneB(q, inst));
-      xb.c = mswz(ulaneC(q, inst));
-    }
+    xb.a = mswz(ulaneA(q, inst));
+    xb.b = mswz(ulaneB(q, inst));
+    xb.c = mswz(ulaneC(q, inst));
     const uint64_t b = tile / tiles_pp;
     const uint64_t piece0 = (tile % tiles_pp) * TILE;
     const uint8_t *P = payloads + b * pstride;
@@ -615,21 +382,11 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     }
 
     // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)
-    if constexpr (kOwn) {
-      lds_barrier();  // the other waves are done reading this region (last tile)
-      stage_own(s, xch, q, inst, wave);
-      lds_barrier();
-      store_own(stg, SH, sstride, 0, nv, piece0, npieces, wave, lane);
-      __builtin_amdgcn_sched_barrier(0);
-    } else if constexpr (kDirect) {
-      store_direct(s, SH, sstride, 0, nv, piece0, npieces, q, inst, wave);
-    } else {
-      lds_barrier();  // previous tile's staging reads are done
-      STAGE(s, stg, q, inst, wave);
-      lds_barrier();
-      STORE(stg, SH, sstride, 0, nv, piece0, npieces, wave, lane);
-      lds_barrier();
-    }
+    lds_barrier();  // the other waves are done reading this region (last tile)
+    stage_own(s, xch, q, inst, wave);
+    lds_barrier();
+    store_own(stg, SH, sstride, 0, nv, piece0, npieces, wave, lane);
+    __builtin_amdgcn_sched_barrier(0);
 
     // ---- IFFT_256 (index 0): passes A (bits 0-2), B (3-5), C (6-7)
     if constexpr (N > 1024) {
@@ -639,10 +396,10 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
       }
     }
     ipass3(s, tabs, posA(q, 0), 0, 0);
-    if constexpr (kOwn) lds_barrier();  // systematic rows read out of the regions
-    exchange<LA, LB>(s, xch, xb, q, inst);
+    lds_barrier();  // systematic rows read out of the regions
+    exchange<LA, LB>(s, xch, xb);
     ipass3(s, tabs, posB(q, 0), 3, 0);
-    exchange<LB, LC>(s, xch, xb, q, inst);
+    exchange<LB, LC>(s, xch, xb);
     ipassC0(s, tabs);
     const State coef = s;
 
@@ -656,26 +413,16 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
 #pragma unroll
         for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(s.l[g][r]), "+v"(s.h[g][r]));
       fpassC(s, tabs, off);
-      if (kOwn) lds_barrier();  // previous coset's rows read out
-      exchange<LC, LB>(s, xch, xb, q, inst);
+      lds_barrier();  // previous coset's rows read out
+      exchange<LC, LB>(s, xch, xb);
       fpass3(s, tabs, posB(q, 0), 3, off);
-      exchange<LB, LA>(s, xch, xb, q, inst);
+      exchange<LB, LA>(s, xch, xb);
       fpass3(s, tabs, posA(q, 0), 0, off);
-      if constexpr (kOwn) {
-        stage_own(s, xch, q, inst, wave);
-        lds_barrier();
-        store_own(stg, SH, sstride, sh, nv, piece0, npieces, wave, lane);
-        __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (kDirect) {
-        store_direct(s, SH, sstride, sh, nv, piece0, npieces, q, inst, wave);
-      } else {
-        lds_barrier();  // all waves done with their exchange regions
-        STAGE(s, stg, q, inst, wave);
-        lds_barrier();
-        STORE(stg, SH, sstride, sh, nv, piece0, npieces, wave, lane);
-        lds_barrier();
-      }
-        };
+      stage_own(s, xch, q, inst, wave);
+      lds_barrier();
+      store_own(stg, SH, sstride, sh, nv, piece0, npieces, wave, lane);
+      __builtin_amdgcn_sched_barrier(0);
+    };
     if constexpr (N == 1024) {
       for (uint32_t sh = K; sh < 1024u && int(sh) < nv; sh += K) coset(sh, sh);
     } else {

@@ -53,7 +53,7 @@ int main() {
   (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_dec_stamp), sizeof(st));
   unsigned long long tot = 0;
   for (int i = 1; i <= 10; ++i) tot += st[i];
-  const char *nm[11] = {"", "sync0", "gather", "sync1", "ifft", "deriv", "fft98", "sync2", "fft7-0", "sync3", "output"};
+  const char *nm[11] = {"", "sync0", "gather", "sync1", "ifft", "deriv", "-", "-", "fft7-0", "-", "output"};
   for (int i = 1; i <= 10; ++i) printf("  %-8s %5.1f%%\n", nm[i], 100.0 * st[i] / tot);
 #endif
   return 0;
