@@ -487,6 +487,8 @@ NPRSResult ECCR_AMD_systematic_batch(unsigned long nv, const uint8_t *d_shards, 
   return result(NPRS_RESULT_OK);
 }
 
+void ECCR_AMD_set_scratch_limit(unsigned long bytes) { set_scratch_limit(bytes); }
+
 const char *ECCR_AMD_last_error(void) { return last_error(); }
 
 }  // extern "C"

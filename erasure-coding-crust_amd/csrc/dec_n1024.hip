@@ -21,17 +21,10 @@
 #include "ec_device.hpp"
 #include "ec_kernels.hpp"
 
-// DEC_ABL: ablation switches for scripts/micro/dec_ablate.cpp only (results are
-// wrong when set): 1 = no phase-1 shard loads, 2 = phase-1 tables from LDS,
-// 4 = no output stores, 8 = no phase-5 shard re-reads, 16 = no E-out table fill,
-// 32 = one table load per FFT pass.
-#ifndef DEC_ABL
-#define DEC_ABL 0
-#endif
-
 namespace ecamd {
-// DEC_STAMP (diagnostic builds only): per-phase s_memtime deltas summed over
-// the waves into g_dec_stamp[phase] (read by scripts/micro/dec_ablate.cpp).
+// DEC_STAMP (diagnostic builds only, never the library): per-phase s_memtime
+// deltas summed over the waves into g_dec_stamp[phase] (read by
+// scripts/micro/dec_ablate.cpp).
 #ifdef DEC_STAMP
 __device__ unsigned long long g_dec_stamp[16];
 #define STAMP(i)                                       \
@@ -91,7 +84,6 @@ __host__ __device__ constexpr uint32_t tlin(uint32_t idx) {
 }
 
 __device__ __forceinline__ void tab_at(const uint8_t *lds, uint32_t lin, Tab &T) {
-  if ((DEC_ABL & 32) && lin > 0x70) return;
 #pragma unroll
   for (int q = 0; q < 5; ++q) {
     const uint4 v = *reinterpret_cast<const uint4 *>(lds + q * Tabs::kPlane + lin);
@@ -252,10 +244,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         const uint8_t *row = SH + uint64_t(v) * sstride + 2 * col0;
         uint32_t w[16];
         const uint64_t avail = slen - 2 * col0;  // bytes of this row inside the tile
-        if (DEC_ABL & 1) {
-#pragma unroll
-          for (int q = 0; q < 16; ++q) w[q] = v * 0x01010101u + q;
-        } else if (avail >= 64) {
+        if (avail >= 64) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const uint4 d = reinterpret_cast<const uint4 *>(row)[q];
@@ -272,8 +261,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
             if (uint64_t(e) < avail) w[e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
         }
         Tab T;
-        if (DEC_ABL & 2) Tabs::load(tabs, v & 1023, T);
-        else load_tab(t.mtab, meta[half] & 0xffffu, T);
+        load_tab(t.mtab, meta[half] & 0xffffu, T);
 #pragma unroll
         for (int g = 0; g < 8; ++g) {  // columns 4g..4g+3: words (h0 l0 h1 l1)(h2 l2 h3 l3)
           const uint32_t a = w[2 * g], c = w[2 * g + 1];
@@ -531,8 +519,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
                             (vperm(ol[1], oh[1], 0x0c0c0400u + 0x0101u * c) << 16);
         const uint32_t w1 = vperm(ol[2], oh[2], 0x0c0c0400u + 0x0101u * c) |
                             (vperm(ol[3], oh[3], 0x0c0c0400u + 0x0101u * c) << 16);
-        if (!(DEC_ABL & 4)) *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);
-        else if (w0 == 0x12345678u && w1 == 0x9abcdef0u) O[0] = 1;  // keep the result live
+        *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);
       }
     }
     STAMP(10);

@@ -29,10 +29,7 @@ namespace ecamd {
 namespace {
 
 using namespace tf;
-#ifndef DEC4_WAVES
-#define DEC4_WAVES 8
-#endif
-constexpr int WAVES = DEC4_WAVES;
+constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
 constexpr int COLS = 4 * WAVES;
 constexpr int LDS_BYTES = Tabs::kBytes + WAVES * REG_BYTES;
@@ -84,9 +81,6 @@ Lin n4096_lin(int nq) {
 // NQ = n / 1024 quarters (2 or 4); K = k = 2^KB (256, 512 or 1024)
 template <int NQ, int KB>
 __global__ void __launch_bounds__(THREADS)
-#if DEC4_WAVES == 4
-__attribute__((amdgpu_waves_per_eu(1, 1)))
-#endif
 reconstruct_n4096(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,

@@ -1,6 +1,7 @@
 // ec_runtime.cpp — device table residency, scratch, per-thread contexts.
 #include "ec_runtime.hpp"
 
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <list>
@@ -133,9 +134,21 @@ hipError_t prepare_kernel(const void *fn, int lds_bytes, int *cus) {
   return hipSuccess;
 }
 
+namespace {
+std::atomic<size_t> g_scratch_limit{0};  // 0 = no limit (ECCR_AMD_set_scratch_limit)
+}
+
+void set_scratch_limit(size_t bytes) { g_scratch_limit = bytes; }
+
 ScratchLease::ScratchLease(DeviceState *d, size_t bytes, hipStream_t stream)
     : d_(d), s_(stream), want_(bytes) {
   if (!d || bytes == 0) return;
+  const size_t limit = g_scratch_limit;
+  if (limit && bytes > limit) {  // as if hipMalloc had failed
+    set_error("erasure_coding_crust(amd): scratch of " + std::to_string(bytes) +
+              " bytes exceeds the limit set by ECCR_AMD_set_scratch_limit");
+    return;
+  }
   d->scratch_mu.lock();
   held_ = true;
   if (d->scratch_cap < bytes) {

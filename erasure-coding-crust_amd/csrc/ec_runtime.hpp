@@ -26,6 +26,9 @@ const uint16_t *device_fold(DeviceState *d, uint32_t n);  // folded LOG_WALSH fo
 // lease is held while a launch is enqueued: it orders the caller's stream
 // after the previous lease's work (an event), so launches from different
 // streams or host threads never overlap on the buffer.
+// Upper bound on one scratch allocation (0 = none): a larger request fails
+// like an out-of-memory hipMalloc (ECCR_AMD_set_scratch_limit).
+void set_scratch_limit(size_t bytes);
 class ScratchLease {
  public:
   ScratchLease(DeviceState *d, size_t bytes, hipStream_t stream);

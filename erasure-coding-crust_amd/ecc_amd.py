@@ -127,6 +127,7 @@ def lib():
             "ECCR_AMD_encode_host_batch": (NPRSResult, [ul, vp, ul, ul, ul, vp, ul, ul]),
             "ECCR_AMD_reconstruct_host_batch": (NPRSResult, [ul, vp, ul, ul, vp, ul, ul, vp, ul,
                                                              ul]),
+            "ECCR_AMD_set_scratch_limit": (None, [ul]),
             "ECCR_AMD_last_error": (C.c_char_p, []),
         }
         for name, (res, args) in sig.items():
@@ -170,6 +171,10 @@ def shard_len(nv: int, payload_len: int) -> int:
 
 def device_count() -> int:
     return int(lib().ECCR_AMD_device_count())
+
+
+def set_scratch_limit(nbytes: int) -> None:
+    lib().ECCR_AMD_set_scratch_limit(nbytes)
 
 
 def last_error() -> str:

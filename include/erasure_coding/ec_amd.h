@@ -140,6 +140,13 @@ struct NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long n_validators,
                                                   unsigned long batch, uint8_t *h_out,
                                                   unsigned long out_stride, unsigned long chunk);
 
+/* Cap on one per-device scratch allocation in bytes (0 = no cap, the
+ * default).  A call whose shape needs more fails with UNKNOWN_CODE_PARAM
+ * (encode) / UNKNOWN_RECONSTRUCTION (reconstruct) exactly as when hipMalloc
+ * runs out of memory; nothing is launched.  For memory-constrained
+ * deployments and the failure-path tests. */
+void ECCR_AMD_set_scratch_limit(unsigned long bytes);
+
 /* Last error message of the calling thread ("" if none). */
 const char *ECCR_AMD_last_error(void);
 

@@ -1,4 +1,4 @@
-// Reconstruct-kernel ablation timer: dec_n1024.hip compiled with -DDEC_ABL=<mask>
+// Reconstruct-kernel timer (+ -DDEC_STAMP phase split): dec_n1024.hip compiled in
 // (switch list there); 512 x 1 MB payloads, n_validators = 1024, 342 present.
 #include "../../erasure-coding-crust_amd/csrc/dec_n1024.hip"
 
@@ -47,7 +47,7 @@ int main() {
   (void)hipEventSynchronize(b);
   float ms = 0;
   (void)hipEventElapsedTime(&ms, a, b);
-  printf("DEC_ABL=%d  %.4f ms per launch (512 x 1 MB)\n", DEC_ABL, ms / reps);
+  printf("reconstruct_n1024  %.4f ms per launch (512 x 1 MB)\n", ms / reps);
 #ifdef DEC_STAMP
   unsigned long long st[16];
   (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_dec_stamp), sizeof(st));

@@ -490,3 +490,108 @@ def test_host_batch_mixed_stream(oracle):
             batch = {15: 64, 300: 32, 5000: 16, 100_000: 8, 1_000_000: 3, 10_000_000: 1}[plen]
             _host_roundtrip(oracle, 1024, plen, batch, 0, seed=1000 * rnd + j,
                             check_all=plen <= 100_000)
+
+
+# ------------------------------------------------------- runtime robustness
+def test_scratch_failure_is_reported(oracle):
+    """A shape whose per-device scratch cannot be had (here: capped below its
+    need, as when hipMalloc fails) returns an error and launches nothing;
+    with the cap lifted the same calls are bit-exact again."""
+    import torch
+    nv, plen = 4096, 30001  # k = 1024 encode keeps its coefficients in scratch
+    p = synth.payload(1, plen).tobytes()
+    E.set_scratch_limit(1024)
+    try:
+        with pytest.raises(E.ECError) as e:
+            E.obtain_chunks(nv, p)
+        assert e.value.tag == E.Tag.UNKNOWN_CODE_PARAM
+        assert "scratch" in E.last_error()
+        sl = E.shard_len(nv, plen)
+        ss = (sl + 15) // 16 * 16
+        d_pay = torch.from_numpy(np.frombuffer(p, np.uint8).copy()).cuda()
+        d_sh = torch.zeros((1, nv, ss), dtype=torch.uint8, device="cuda")
+        with pytest.raises(E.ECError):
+            E.encode_batch(nv, d_pay, plen, plen, 1, d_sh, ss)
+        # n = 65536 reconstruct runs the generic kernel with global scratch
+        nv2 = 65536
+        n2, k2, _ = E.code_params(nv2)
+        sh2 = oracle.encode(nv2, synth.payload(2, 3 * k2 + 1).tobytes())
+        with pytest.raises(E.ECError) as e2:
+            E.reconstruct(nv2, [(i, sh2[i]) for i in range(k2, 2 * k2)])
+        assert e2.value.tag == E.Tag.UNKNOWN_RECONSTRUCTION
+    finally:
+        E.set_scratch_limit(0)
+    assert E.obtain_chunks(nv, p) == oracle.encode(nv, p)
+
+
+def test_thread_exit_releases_contexts():
+    """Each host thread's C-ABI context (stream, pinned and device staging) is
+    released when the thread exits: many short-lived threads leave device
+    memory where it was."""
+    import threading
+    import torch
+    nv, plen = 1024, 1_000_000
+    p = synth.payload(3, plen).tobytes()
+    n, k, thr = E.code_params(nv)
+    keep = set(int(x) for x in synth.present_set(5, nv, thr))
+
+    def one():
+        sh = E.obtain_chunks(nv, p)
+        assert E.reconstruct(nv, [(i, sh[i]) for i in sorted(keep)])[:plen] == p
+
+    t = threading.Thread(target=one)  # warm the per-device state
+    t.start()
+    t.join()
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    for _ in range(48):
+        t = threading.Thread(target=one)
+        t.start()
+        t.join()
+    torch.cuda.synchronize()
+    free1 = torch.cuda.mem_get_info()[0]
+    # each context holds >= 9 MB of device staging (4 MB shards in, 4 MB out, 1 MB payload)
+    assert free0 - free1 < 64 << 20, (free0, free1)
+
+
+FIRST_CALLS = r'''
+import sys, threading
+sys.path[:0] = [{pkg!r}, {orc!r}]
+import ecc_amd as E, oracle, synth
+o = oracle.Oracle()
+cases = [(1024, 40001), (4096, 30001), (600, 20001), (1500, 20001), (2500, 20001), (100, 9999), (20, 999), (3070, 30001)]
+want = {{}}
+for nv, plen in cases:
+    p = synth.payload(nv, plen).tobytes()
+    want[nv] = (p, b"".join(o.encode(nv, p)))
+go = threading.Barrier(len(cases))
+bad = []
+def worker(nv):
+    p, ref = want[nv]
+    go.wait()  # every thread makes its first library call at once
+    sh = E.obtain_chunks(nv, p)
+    if b"".join(sh) != ref:
+        bad.append(("encode", nv))
+        return
+    n, k, thr = E.code_params(nv)
+    keep = sorted(int(x) for x in synth.present_set(nv + 1, nv, thr))
+    if E.reconstruct(nv, [(i, sh[i]) for i in keep])[:len(p)] != p:
+        bad.append(("reconstruct", nv))
+ts = [threading.Thread(target=worker, args=(nv,)) for nv, _ in cases]
+[t.start() for t in ts]
+[t.join(240) for t in ts]
+print("BAD", bad)
+sys.exit(1 if bad or any(t.is_alive() for t in ts) else 0)
+'''
+
+
+def test_fresh_process_concurrent_first_calls():
+    """In a fresh process, threads make their FIRST library calls at the same
+    moment, over shapes that use every specialised kernel (their per-device
+    first-call setup races): all results equal the oracle's (ADVICE r01)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = FIRST_CALLS.format(pkg=os.path.join(root, "erasure-coding-crust_amd"),
+                              orc=os.path.join(root, "oracle"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
