@@ -56,9 +56,25 @@ static_assert(OutTabs::kBytes <= WAVES * REG_BYTES, "output tables fit the regio
 // region address of position v: 8-byte slots XOR-swizzled so that every
 // access pattern used below (positions varying in bits 4-8, 0-3+8, 0-4) is
 // bank-conflict free
-__device__ __forceinline__ uint32_t raddr(uint32_t v) {
+__host__ __device__ constexpr uint32_t raddr(uint32_t v) {
   const uint32_t f = (v & 31) ^ ((v >> 4) & 31);
   return ((v >> 5) << 8) | (f << 3);
+}
+
+// raddr is GF(2)-linear in v, so a wave's region access for position
+// (lane part) | (register part) is one v_xor of a per-lane LDS address with a
+// compile-time constant.  The region base (a multiple of 8 KB) has no bits in
+// common with raddr (< 8 KB), so it folds into the per-lane address too.
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+__device__ __forceinline__ uint32_t lds_addr(const uint8_t *p) {
+  return uint32_t(uintptr_t((const lds_u8 *)p));
+}
+__device__ __forceinline__ uint2 lds_ld2(uint32_t a) {
+  const uint64_t v = *(const __attribute__((address_space(3))) uint64_t *)(uintptr_t(a));
+  return make_uint2(uint32_t(v), uint32_t(v >> 32));
+}
+__device__ __forceinline__ void lds_st2(uint32_t a, uint2 v) {
+  *(__attribute__((address_space(3))) uint64_t *)(uintptr_t(a)) = (uint64_t(v.y) << 32) | v.x;
 }
 
 __device__ __forceinline__ uint32_t skew_idx(uint32_t pos_a, int m) {
@@ -309,41 +325,39 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     // ---- phase 2: IFFT_1024 on this wave's group
     S16 s;
     {  // layout A: v = 16*lane + r
+      const uint32_t la = lds_addr(my) | raddr(16 * lane);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(16 * lane + r));
+        const uint2 x = lds_ld2(la ^ raddr(r));
         s.l[r] = x.x;
         s.h[r] = x.y;
       }
       ipass4<0>(s, tabs, tlin(16 * lane));
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        *reinterpret_cast<uint2 *>(my + raddr(16 * lane + r)) = make_uint2(s.l[r], s.h[r]);
+      for (int r = 0; r < 16; ++r) lds_st2(la ^ raddr(r), make_uint2(s.l[r], s.h[r]));
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
     const uint32_t baseB = (lane & 15) | ((lane >> 4) << 8);  // layout B: bits 4-7 in registers
     {
+      const uint32_t lb = lds_addr(my) | raddr(baseB);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(baseB | (r << 4)));
+        const uint2 x = lds_ld2(lb ^ raddr(uint32_t(r) << 4));
         s.l[r] = x.x;
         s.h[r] = x.y;
       }
       ipass4<4>(s, tabs, tlin((lane >> 4) << 8));
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        *reinterpret_cast<uint2 *>(my + raddr(baseB | (r << 4))) = make_uint2(s.l[r], s.h[r]);
+      for (int r = 0; r < 16; ++r) lds_st2(lb ^ raddr(uint32_t(r) << 4), make_uint2(s.l[r], s.h[r]));
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
     // layout C: r bit0 = p8, bit1 = p9, bit2 = p6, bit3 = p7; lane = p0..p5
-    auto posC = [&](int r) {
-      return lane | (uint32_t((r >> 2) & 3) << 6) | (uint32_t(r & 3) << 8);
-    };
+    const uint32_t lc = lds_addr(my) | raddr(lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(posC(r)));
+      const uint2 x = lds_ld2(lc ^ raddr((uint32_t((r >> 2) & 3) << 6) | (uint32_t(r & 3) << 8)));
       s.l[r] = x.x;
       s.h[r] = x.y;
     }

@@ -131,7 +131,12 @@ def lib():
             "ECCR_AMD_last_error": (C.c_char_p, []),
         }
         for name, (res, args) in sig.items():
-            f = getattr(L, name)
+            try:
+                f = getattr(L, name)
+            except AttributeError:
+                if os.environ.get("ECC_AMD_LIB"):  # an older A/B build: newer symbols absent
+                    continue
+                raise
             f.restype = res
             f.argtypes = args
         _lib = L
