@@ -212,11 +212,14 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
 
     // ---- IFFT_n, derivative, FFT_n (back to layout A)
     S16 s;
+    {
+      const uint32_t la = region_lane<LA>(my, lane);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(posA(lane, r)));
-      s.l[r] = x.x;
-      s.h[r] = x.y;
+      for (int r = 0; r < 16; ++r) {
+        const uint2 x = lds_ld2(region_at<LA>(la, r));
+        s.l[r] = x.x;
+        s.h[r] = x.y;
+      }
     }
     // table addresses are recomputed from an opaque lane for every pass: the
     // compiler would otherwise keep each pass's ~40 addresses live (spilled)

@@ -63,19 +63,9 @@ __host__ __device__ constexpr uint32_t raddr(uint32_t v) {
 
 // raddr is GF(2)-linear in v, so a wave's region access for position
 // (lane part) | (register part) is one v_xor of a per-lane LDS address with a
-// compile-time constant.  The region base (a multiple of 8 KB) has no bits in
-// common with raddr (< 8 KB), so it folds into the per-lane address too.
-typedef __attribute__((address_space(3))) uint8_t lds_u8;
-__device__ __forceinline__ uint32_t lds_addr(const uint8_t *p) {
-  return uint32_t(uintptr_t((const lds_u8 *)p));
-}
-__device__ __forceinline__ uint2 lds_ld2(uint32_t a) {
-  const uint64_t v = *(const __attribute__((address_space(3))) uint64_t *)(uintptr_t(a));
-  return make_uint2(uint32_t(v), uint32_t(v >> 32));
-}
-__device__ __forceinline__ void lds_st2(uint32_t a, uint2 v) {
-  *(__attribute__((address_space(3))) uint64_t *)(uintptr_t(a)) = (uint64_t(v.y) << 32) | v.x;
-}
+// compile-time constant (lds_addr / lds_ld2 / lds_st2, ec_device.hpp).  The
+// region base (a multiple of 8 KB) has no bits in common with raddr (< 8 KB),
+// so it folds into the per-lane address too.
 
 __device__ __forceinline__ uint32_t skew_idx(uint32_t pos_a, int m) {
   const uint32_t d = 1u << m;

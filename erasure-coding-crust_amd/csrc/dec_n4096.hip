@@ -177,9 +177,10 @@ reconstruct_n4096(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // table image landed
       lds_barrier();
       __builtin_amdgcn_sched_barrier(0);
+      const uint32_t la = region_lane<LA>(my, lq);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(posA(lq, r)));
+        const uint2 x = lds_ld2(region_at<LA>(la, r));
         Qq.l[r] = x.x;
         Qq.h[r] = x.y;
       }

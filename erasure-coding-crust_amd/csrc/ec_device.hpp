@@ -49,6 +49,22 @@ __device__ __forceinline__ void load_row_tail64(const uint8_t *row, uint64_t ava
   }
 }
 
+// 32-bit LDS address of an LDS pointer, and 8-byte accesses at such an
+// address.  For GF(2)-linear swizzles: an access at (per-lane part) XOR
+// (compile-time part) is then one v_xor (the compiler does not see the
+// linearity through pointer arithmetic and emits ~4 VALU per access).
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+__device__ __forceinline__ uint32_t lds_addr(const uint8_t *p) {
+  return uint32_t(uintptr_t((const lds_u8 *)p));
+}
+__device__ __forceinline__ uint2 lds_ld2(uint32_t a) {
+  const uint64_t v = *(const __attribute__((address_space(3))) uint64_t *)(uintptr_t(a));
+  return make_uint2(uint32_t(v), uint32_t(v >> 32));
+}
+__device__ __forceinline__ void lds_st2(uint32_t a, uint2 v) {
+  *(__attribute__((address_space(3))) uint64_t *)(uintptr_t(a)) = (uint64_t(v.y) << 32) | v.x;
+}
+
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();

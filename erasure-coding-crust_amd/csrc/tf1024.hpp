@@ -26,7 +26,7 @@ struct S16 {
   uint32_t l[16], h[16];
 };
 
-__device__ __forceinline__ uint32_t raddr(uint32_t v) {
+__host__ __device__ constexpr uint32_t raddr(uint32_t v) {
   const uint32_t f = (v & 31) ^ ((v >> 4) & 31);
   return ((v >> 5) << 8) | (f << 3);
 }
@@ -173,35 +173,48 @@ __device__ __forceinline__ void fpassC0(S16 &s, const uint8_t *tabs) {
   for (int hi = 0; hi < 4; ++hi) fb(s, 4 * hi + 2, 4 * hi + 3, Ta);
 }
 
-__device__ __forceinline__ uint32_t posA(uint32_t lane, int r) { return 16 * lane + uint32_t(r); }
-__device__ __forceinline__ uint32_t posB(uint32_t lane, int r) {
+__host__ __device__ constexpr uint32_t posA(uint32_t lane, int r) { return 16 * lane + uint32_t(r); }
+__host__ __device__ constexpr uint32_t posB(uint32_t lane, int r) {
   return (lane & 15) | (uint32_t(r) << 4) | ((lane >> 4) << 8);
 }
-__device__ __forceinline__ uint32_t posC(uint32_t lane, int r) {
+__host__ __device__ constexpr uint32_t posC(uint32_t lane, int r) {
   return lane | (uint32_t((r >> 2) & 3) << 6) | (uint32_t(r & 3) << 8);
 }
 
 enum Layout { LA, LB, LC };
 
 template <Layout L>
-__device__ __forceinline__ uint32_t pos_of(uint32_t lane, int r) {
+__host__ __device__ constexpr uint32_t pos_of(uint32_t lane, int r) {
   if constexpr (L == LA) return posA(lane, r);
   else if constexpr (L == LB) return posB(lane, r);
   else return posC(lane, r);
+}
+
+// LDS address of position pos_of<X>(lane, r) in the wave's region `my`
+// (8 KB aligned): raddr is GF(2)-linear and the lane and register parts of a
+// position are disjoint, so it is (per-lane address) ^ (constant of r)
+template <Layout X>
+__device__ __forceinline__ uint32_t region_lane(const uint8_t *my, uint32_t lane) {
+  return lds_addr(my) | raddr(pos_of<X>(lane, 0));
+}
+template <Layout X>
+__device__ __forceinline__ uint32_t region_at(uint32_t lane_addr, int r) {
+  return lane_addr ^ raddr(pos_of<X>(0, r));
 }
 
 // wave-private exchange of the 16 registers from layout FROM to layout TO
 template <Layout FROM, Layout TO>
 __device__ __forceinline__ void exchange(S16 &s, uint8_t *my, uint32_t lane) {
   asm volatile("" : "+v"(lane));  // addresses computed here, not hoisted and kept live
+  const uint32_t af = region_lane<FROM>(my, lane);
 #pragma unroll
-  for (int r = 0; r < 16; ++r)
-    *reinterpret_cast<uint2 *>(my + raddr(pos_of<FROM>(lane, r))) = make_uint2(s.l[r], s.h[r]);
+  for (int r = 0; r < 16; ++r) lds_st2(region_at<FROM>(af, r), make_uint2(s.l[r], s.h[r]));
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
+  const uint32_t at = region_lane<TO>(my, lane);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const uint2 x = *reinterpret_cast<const uint2 *>(my + raddr(pos_of<TO>(lane, r)));
+    const uint2 x = lds_ld2(region_at<TO>(at, r));
     s.l[r] = x.x;
     s.h[r] = x.y;
   }
