@@ -176,10 +176,43 @@ __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ?
 
 }  // namespace
 
+// Gather order of a payload's 1024 received rows (its erasure pattern): the
+// present rows first, then the absent ones, dealt round-robin over the 8
+// waves (slot s of each half -> wave s % 8, lane s / 8), stored in the order
+// threads read it: entry [half * 512 + tid] = (row << 16) | mul_index(E[row])
+// for a present row, (row << 16) | 0xFFFF for an absent one.  A wave whose
+// slots of a half are all absent then skips that half's multiplies (uniform
+// branch); with 1/3 of the rows present (threshold) that is every wave's
+// second half, where the natural row order multiplied in every wave.
+__global__ void __launch_bounds__(1024) n1024_order(const uint8_t *__restrict__ present,
+                                                    const uint16_t *__restrict__ elog,
+                                                    const uint32_t *__restrict__ pattern, int nv,
+                                                    uint32_t *__restrict__ order) {
+  __shared__ uint32_t cnt[16];
+  const uint32_t b = blockIdx.x, v = threadIdx.x, lane = v & 63, w = v >> 6;
+  const uint64_t pt = pattern ? pattern[b] : b;
+  const bool f = int(v) < nv && present[pt * N + v] != 0;
+  const uint64_t m = __ballot(f);
+  const uint32_t below = __popcll(m & ((1ull << lane) - 1));
+  if (lane == 0) cnt[w] = uint32_t(__popcll(m));
+  __syncthreads();
+  uint32_t pw = 0, c = 0;  // present rows in earlier waves, and in all
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    pw += i < int(w) ? cnt[i] : 0u;
+    c += cnt[i];
+  }
+  // slot: present rows in row order, then absent rows in row order
+  const uint32_t slot = f ? pw + below : c + (64 * w - pw) + (lane - below);
+  const uint32_t half = slot >> 9, sp = slot & 511;
+  const uint32_t t = (sp & 7) * 64 + (sp >> 3);
+  order[uint64_t(b) * N + half * 512 + t] = (v << 16) | (f ? mul_index(elog[pt * N + v]) : 0xFFFFu);
+}
+
 __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
-    const uint32_t *__restrict__ pattern,
+    const uint32_t *__restrict__ pattern, const uint32_t *__restrict__ order,
     uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t batch, DevTables t) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
@@ -196,21 +229,16 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   const uint64_t ncols = slen / 2;
   const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);
   const uint64_t total = uint64_t(tiles_pp) * batch;
-  // per-row metadata of rows v = tid, tid + 512 of a tile's payload: bit 16 =
-  // present (and < nv), bits 0-15 = mul_index(E[v]).  Loaded one tile ahead so
-  // the gather's table loads and the output-table fill wait on one global
-  // latency instead of two (present/E, then the table).
+  // m[0], m[1]: this thread's two gather slots (n1024_order): row << 16 |
+  // mul_index(E[row]), low half 0xFFFF = absent.  Loaded one tile ahead so the
+  // gather's table loads wait on one global latency instead of two.
   // m[2], m[3]: the output rows y = 4 lane + q (q = 0..3) of phase 5, 16 bits
   // each: 0xFFFF = present (copied from the shard), else mul_index(E[y]) (the
   // erased value is scaled by E[y]; y < 256 < nv always holds for n = 1024).
   auto load_meta = [&](uint64_t tl, uint32_t tid, uint32_t (&m)[4]) {
     const uint64_t bb = tl / tiles_pp, pt = pattern ? pattern[bb] : bb;
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const uint32_t v = tid + half * THREADS;
-      const uint32_t p = present[pt * N + v], e = elog[pt * N + v];
-      m[half] = mul_index(e) | ((p != 0 && int(v) < nv) ? 0x10000u : 0u);
-    }
+    for (int half = 0; half < 2; ++half) m[half] = order[bb * N + half * THREADS + tid];
     const uint32_t y0 = 4 * (tid & 63);
     const uint32_t p4 = *reinterpret_cast<const uint32_t *>(present + pt * N + y0);
     const uint2 e4 = *reinterpret_cast<const uint2 *>(elog + pt * N + y0);
@@ -236,17 +264,18 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
     uint8_t *O = out + b * ostride;
 
-    // ---- phase 1: gather + scale rows v = tid, tid + 512 (decode_main:174-177)
+    // ---- phase 1: gather + scale this thread's two slots' rows (present rows
+    // first, n1024_order; decode_main:174-177); absent rows are written as 0
     STAMP(0);
     __syncthreads();  // previous tile's readers of the regions are done
     STAMP(1);
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
-      const uint32_t v = tid + half * THREADS;
+      const uint32_t v = meta[half] >> 16;
       uint32_t l[8], h[8];
 #pragma unroll
       for (int g = 0; g < 8; ++g) l[g] = h[g] = 0;
-      if (meta[half] & 0x10000u) {
+      if ((meta[half] & 0xffffu) != 0xffffu) {
         const uint8_t *row = SH + uint64_t(v) * sstride + 2 * col0;
         uint32_t w[16];
         const uint64_t avail = slen - 2 * col0;  // bytes of this row inside the tile
@@ -542,18 +571,25 @@ hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
                                     const uint8_t *d_shards, size_t slen, size_t sstride,
                                     const uint8_t *d_present, const uint16_t *d_err_log,
                                     const uint32_t *d_pattern,
-                                    size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
+                                    size_t batch, uint8_t *d_out, size_t ostride, void *scratch,
+                                    hipStream_t s) {
   int cus = 0;
   if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&reconstruct_n1024),
                                           LDS_BYTES, &cus);
       e != hipSuccess)
     return e;
+  if (!scratch) return hipErrorInvalidValue;
+  uint32_t *order = static_cast<uint32_t *>(scratch);  // n1024_scratch_bytes(batch)
+  hipLaunchKernelGGL(n1024_order, dim3(unsigned(batch)), dim3(1024), 0, s, d_present, d_err_log,
+                     d_pattern, int(p.nv), order);
   const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   hipLaunchKernelGGL(reconstruct_n1024, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
-                     uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, d_out,
-                     uint64_t(ostride), int(p.nv), uint32_t(batch), t);
+                     uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, order,
+                     d_out, uint64_t(ostride), int(p.nv), uint32_t(batch), t);
   return hipGetLastError();
 }
+
+size_t n1024_scratch_bytes(size_t batch) { return batch * N * sizeof(uint32_t); }
 
 }  // namespace ecamd

@@ -85,12 +85,15 @@ hipError_t launch_encode_gen(const CodeParams &p, const DevTables &t, const uint
                              size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                              size_t sstride, hipStream_t s);
 
-// specialised kernels (dec_n1024.hip)
+// specialised kernels (dec_n1024.hip); scratch: n1024_scratch_bytes(batch)
+// (each payload's gather order)
 bool n1024_applicable(const CodeParams &p);
+size_t n1024_scratch_bytes(size_t batch);
 hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
                                     const uint8_t *d_shards, size_t slen, size_t sstride,
                                     const uint8_t *d_present, const uint16_t *d_err_log,
-                                    const uint32_t *d_pattern, size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s);
+                                    const uint32_t *d_pattern, size_t batch, uint8_t *d_out,
+                                    size_t ostride, void *scratch, hipStream_t s);
 
 // specialised kernels (dec_n4096.hip)
 bool n4096_applicable(const CodeParams &p);

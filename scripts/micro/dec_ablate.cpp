@@ -36,13 +36,15 @@ int main() {
   (void)hipMemset(sh, 0x3c, B * 1024 * ss);
   (void)hipMemcpy(dp, pres.data(), pres.size(), hipMemcpyHostToDevice);
   (void)hipMemcpy(de, el.data(), el.size() * 2, hipMemcpyHostToDevice);
+  void *order = nullptr;
+  (void)hipMalloc(&order, n1024_scratch_bytes(B));
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
-  for (int i = 0; i < 2; ++i) launch_reconstruct_n1024(p, t, sh, sl, ss, dp, de, nullptr, B, out, sl * 256, nullptr);
+  for (int i = 0; i < 2; ++i) launch_reconstruct_n1024(p, t, sh, sl, ss, dp, de, nullptr, B, out, sl * 256, order, nullptr);
   (void)hipEventRecord(a);
   const int reps = 10;
-  for (int i = 0; i < reps; ++i) launch_reconstruct_n1024(p, t, sh, sl, ss, dp, de, nullptr, B, out, sl * 256, nullptr);
+  for (int i = 0; i < reps; ++i) launch_reconstruct_n1024(p, t, sh, sl, ss, dp, de, nullptr, B, out, sl * 256, order, nullptr);
   (void)hipEventRecord(b);
   (void)hipEventSynchronize(b);
   float ms = 0;
