@@ -1,5 +1,5 @@
 set -u
 cd scripts/micro
-for b in dec_abl_0 dec_abl_1 dec_abl_2 dec_stamp dec_abl_0; do
+for b in dec_abl_0 dec_stamp enc_abl_0; do
   timeout -k 10 60 ./$b || exit 1
 done
