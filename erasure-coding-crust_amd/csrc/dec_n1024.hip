@@ -411,26 +411,39 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     //   c'[y] = c0[y] ^ c1[y] ^ c2[y] ^ XOR_{b < 8, y_b = 0} c0[y | 2^b]
     // with c0 / c1 / c2 = registers 4 q / 4 q + 1 / 4 q + 2 (p8 p9 = 00 / 10 /
     // 01), q bit 0 = p6, bit 1 = p7, lane bits = p0..p5.
+    // Lane-bit terms (lanes with p_b = 0 add the value of lane + 2^b): p2, p3
+    // by one row_shl DPP xor each whose bank mask leaves the p_b = 1 lanes
+    // untouched; p0, p1 by quad_perm DPP xors that hand the p_b = 1 lanes
+    // their own c0 instead of 0 (corrected once: c0 is kept where p0 ^ p1 = 0
+    // rather than xor'ed twice); p4, p5 by permlane swaps, masked.
     uint32_t ql[4], qh[4];
+    {
+      const uint32_t keep0 = ((lane ^ (lane >> 1)) & 1) ? 0u : 0xffffffffu;
+      const uint32_t m4 = ((lane >> 4) & 1) ? 0u : 0xffffffffu;
+      const uint32_t m5 = ((lane >> 5) & 1) ? 0u : 0xffffffffu;
+      const auto lane_terms = [&](uint32_t c0, uint32_t acc) {
+        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(c0), 0xF5, 0xf, 0xf, false));  // quad [1,1,3,3]
+        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(c0), 0xEE, 0xf, 0xf, false));  // quad [2,3,2,3]
+        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(c0), 0x104, 0xf, 0x5, false));  // row_shl:4, banks 0, 2
+        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(c0), 0x108, 0xf, 0x3, false));  // row_shl:8, banks 0, 1
+        acc = __builtin_amdgcn_bitop3_b32(acc, from_upper(c0, 4), m4, 0x78);  // acc ^ (x & m)
+        acc = __builtin_amdgcn_bitop3_b32(acc, from_upper(c0, 5), m5, 0x78);
+        return __builtin_amdgcn_bitop3_b32(acc, c0, keep0, 0x78);
+      };
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t al = s.l[4 * q + 1] ^ s.l[4 * q + 2], ah = s.h[4 * q + 1] ^ s.h[4 * q + 2];
-#pragma unroll
-      for (int lb = 0; lb < 6; ++lb) {  // lane bits 0..5 = p0..p5
-        const uint32_t m = ((lane >> lb) & 1) ? 0u : 0xffffffffu;
-        al ^= from_upper(s.l[4 * q], lb) & m;
-        ah ^= from_upper(s.h[4 * q], lb) & m;
+      for (int q = 0; q < 4; ++q) {
+        uint32_t al = s.l[4 * q + 1] ^ s.l[4 * q + 2], ah = s.h[4 * q + 1] ^ s.h[4 * q + 2];
+        if (!(q & 1)) {  // p6 = 0
+          al ^= s.l[4 * (q | 1)];
+          ah ^= s.h[4 * (q | 1)];
+        }
+        if (!(q & 2)) {  // p7 = 0
+          al ^= s.l[4 * (q | 2)];
+          ah ^= s.h[4 * (q | 2)];
+        }
+        ql[q] = lane_terms(s.l[4 * q], al);
+        qh[q] = lane_terms(s.h[4 * q], ah);
       }
-      if (!(q & 1)) {  // p6 = 0
-        al ^= s.l[4 * (q | 1)];
-        ah ^= s.h[4 * (q | 1)];
-      }
-      if (!(q & 2)) {  // p7 = 0
-        al ^= s.l[4 * (q | 2)];
-        ah ^= s.h[4 * (q | 2)];
-      }
-      ql[q] = s.l[4 * q] ^ al;
-      qh[q] = s.h[4 * q] ^ ah;
     }
     STAMP(5);
     STAMP(6);
