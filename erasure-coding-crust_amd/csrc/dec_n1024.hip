@@ -265,9 +265,39 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     uint8_t *O = out + b * ostride;
 
     // ---- phase 1: gather + scale this thread's two slots' rows (present rows
-    // first, n1024_order; decode_main:174-177); absent rows are written as 0
+    // first, n1024_order; decode_main:174-177); absent rows are written as 0.
+    // The first slot's row and E[v] table are requested before the barrier
+    // (they only land in registers), so their latency overlaps the wait for
+    // the other waves' previous tile; the second slot (mostly absent rows:
+    // present rows come first) is loaded after it.
+    uint32_t w[2][16];
+    Tab RT[2];
+    const uint64_t avail = slen - 2 * col0;  // bytes of a row inside the tile
+    const auto load_row = [&](int half) __attribute__((always_inline)) {
+      {
+        const uint8_t *row = SH + uint64_t(meta[half] >> 16) * sstride + 2 * col0;
+        if (avail >= 64) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint4 d = reinterpret_cast<const uint4 *>(row)[q];
+            w[half][4 * q] = d.x;
+            w[half][4 * q + 1] = d.y;
+            w[half][4 * q + 2] = d.z;
+            w[half][4 * q + 3] = d.w;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) w[half][q] = 0;
+#pragma unroll
+          for (int e = 0; e < 64; ++e)  // constant trip count: w stays in registers
+            if (uint64_t(e) < avail) w[half][e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
+        }
+        load_tab(t.mtab, meta[half] & 0xffffu, RT[half]);
+      }
+    };
+    if ((meta[0] & 0xffffu) != 0xffffu) load_row(0);
     STAMP(0);
-    __syncthreads();  // previous tile's readers of the regions are done
+    lds_barrier();  // previous tile's readers of the regions are done (LDS only)
     STAMP(1);
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -276,32 +306,12 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
 #pragma unroll
       for (int g = 0; g < 8; ++g) l[g] = h[g] = 0;
       if ((meta[half] & 0xffffu) != 0xffffu) {
-        const uint8_t *row = SH + uint64_t(v) * sstride + 2 * col0;
-        uint32_t w[16];
-        const uint64_t avail = slen - 2 * col0;  // bytes of this row inside the tile
-        if (avail >= 64) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint4 d = reinterpret_cast<const uint4 *>(row)[q];
-            w[4 * q] = d.x;
-            w[4 * q + 1] = d.y;
-            w[4 * q + 2] = d.z;
-            w[4 * q + 3] = d.w;
-          }
-        } else {
-#pragma unroll
-          for (int q = 0; q < 16; ++q) w[q] = 0;
-#pragma unroll
-          for (int e = 0; e < 64; ++e)  // constant trip count: w stays in registers
-            if (uint64_t(e) < avail) w[e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
-        }
-        Tab T;
-        load_tab(t.mtab, meta[half] & 0xffffu, T);
+        if (half == 1) load_row(1);
 #pragma unroll
         for (int g = 0; g < 8; ++g) {  // columns 4g..4g+3: words (h0 l0 h1 l1)(h2 l2 h3 l3)
-          const uint32_t a = w[2 * g], c = w[2 * g + 1];
+          const uint32_t a = w[half][2 * g], c = w[half][2 * g + 1];
           const uint32_t xh = vperm(c, a, 0x06040200u), xl = vperm(c, a, 0x07050301u);
-          mul_acc(xl, xh, T, l[g], h[g]);
+          mul_acc(xl, xh, RT[half], l[g], h[g]);
         }
       }
 #pragma unroll
