@@ -128,45 +128,51 @@ reconstruct_n4096(
     const auto quarter = [&](const int q) __attribute__((always_inline)) {
       S16 Qq;
       __builtin_amdgcn_sched_barrier(0);
-      lds_barrier();  // every wave is done with the tables and its region
       uint32_t tq = tid;
       asm volatile("" : "+v"(tq));  // this quarter's addresses and loads are not hoisted above here
       const uint32_t lq = tq & 63;
+      // gather + scale the quarter's present rows (decode_main:174-177) into
+      // the 8 groups' regions: thread -> rows 1024q + tid, + 512.  The first
+      // row and its E[v] table are requested before the barrier (registers
+      // only), so their latency overlaps the wait for the other waves.
+      uint32_t w[1024 / THREADS][16];
+      Tab RT[1024 / THREADS];
+      const uint64_t avail = slen - 2 * col0;
+      const auto load_row = [&](int half) __attribute__((always_inline)) {
+        const uint8_t *row = SH + uint64_t(1024 * q + tq + half * THREADS) * sstride + 2 * col0;
+        if (avail >= 64) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint4 d = reinterpret_cast<const uint4 *>(row)[j];
+            w[half][4 * j] = d.x;
+            w[half][4 * j + 1] = d.y;
+            w[half][4 * j + 2] = d.z;
+            w[half][4 * j + 3] = d.w;
+          }
+        } else {
+          load_row_tail64(row, avail, w[half]);
+        }
+        load_tab(t.mtab, mq[half] & 0xffffu, RT[half]);
+      };
+      if (mq[0] & 0x10000u) load_row(0);
+      lds_barrier();  // every wave is done with the tables and its region
       // the quarter's tables (skews 1024q + i) by LDS-DMA, in the background
       // of the row gather; retired before the barrier below
       Tabs::dma_image<THREADS>(tabs, t.timg + q * kTabImageBytes, tq);
       __builtin_amdgcn_sched_barrier(0);
-      // gather + scale the quarter's present rows (decode_main:174-177) into
-      // the 8 groups' regions: thread -> rows 1024q + tid, + 512
 #pragma unroll
       for (int half = 0; half < 1024 / THREADS; ++half) {
-        const uint32_t vl = tq + half * THREADS, v = 1024 * q + vl;
+        const uint32_t vl = tq + half * THREADS;
         uint32_t l[8], h[8];
 #pragma unroll
         for (int g = 0; g < 8; ++g) l[g] = h[g] = 0;
         if (mq[half] & 0x10000u) {
-          const uint8_t *row = SH + uint64_t(v) * sstride + 2 * col0;
-          uint32_t w[16];
-          const uint64_t avail = slen - 2 * col0;
-          if (avail >= 64) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const uint4 d = reinterpret_cast<const uint4 *>(row)[j];
-              w[4 * j] = d.x;
-              w[4 * j + 1] = d.y;
-              w[4 * j + 2] = d.z;
-              w[4 * j + 3] = d.w;
-            }
-          } else {
-            load_row_tail64(row, avail, w);
-          }
-          Tab T;
-          load_tab(t.mtab, mq[half] & 0xffffu, T);
+          if (half > 0) load_row(half);
 #pragma unroll
           for (int g = 0; g < 8; ++g) {
-            const uint32_t a = w[2 * g], c = w[2 * g + 1];
+            const uint32_t a = w[half][2 * g], c = w[half][2 * g + 1];
             const uint32_t xh = vperm(c, a, 0x06040200u), xl = vperm(c, a, 0x07050301u);
-            mul_acc(xl, xh, T, l[g], h[g]);
+            mul_acc(xl, xh, RT[half], l[g], h[g]);
           }
         }
 #pragma unroll
