@@ -49,9 +49,19 @@ using Tabs = LdsTabs<1024>;
 using OutTabs = LdsTabs<256>;  // output multiply tables E[y], y < 256 (in the regions)
 constexpr int TAB_REGION = Tabs::kBytes;
 constexpr int REG_BYTES = N * 8;  // one wave's group: 1024 x uint2
-constexpr int LDS_BYTES = TAB_REGION + WAVES * REG_BYTES;
+// received rows y < K of the tile as read (the present ones): phase 5 copies
+// them to the output instead of re-reading them from HBM
+constexpr int STAGE_BYTES = K * COLS * 2;
+constexpr int LDS_BYTES = TAB_REGION + WAVES * REG_BYTES + STAGE_BYTES;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 static_assert(OutTabs::kBytes <= WAVES * REG_BYTES, "output tables fit the regions");
+
+// staging address of (row y < K, group g): the 8 bytes of columns 4g..4g+3 in
+// 32-byte chunks of 4 rows; chunk g of 4-row block y/4 is swizzled by (y/4) & 7
+// so the phase-5 reads (lane = y/4, 32 B each, fixed g) cover all banks
+__device__ __forceinline__ uint32_t stage_addr(uint32_t y, uint32_t g) {
+  return ((y >> 2) << 8) | ((g ^ ((y >> 2) & 7)) << 5) | ((y & 3) << 3);
+}
 
 // region address of position v: 8-byte slots XOR-swizzled so that every
 // access pattern used below (positions varying in bits 4-8, 0-3+8, 0-4) is
@@ -217,6 +227,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
   uint8_t *regions = lds + TAB_REGION;
+  uint8_t *stage = regions + WAVES * REG_BYTES;
   const uint32_t tid0 = threadIdx.x, wave = tid0 >> 6;
   uint8_t *my = regions + wave * REG_BYTES;
 
@@ -307,6 +318,11 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       for (int g = 0; g < 8; ++g) l[g] = h[g] = 0;
       if ((meta[half] & 0xffffu) != 0xffffu) {
         if (half == 1) load_row(1);
+        if (v < uint32_t(K)) {  // a present data row: kept for phase 5
+#pragma unroll
+          for (int g = 0; g < 8; ++g)
+            *reinterpret_cast<uint2 *>(stage + stage_addr(v, g)) = make_uint2(w[half][2 * g], w[half][2 * g + 1]);
+        }
 #pragma unroll
         for (int g = 0; g < 8; ++g) {  // columns 4g..4g+3: words (h0 l0 h1 l1)(h2 l2 h3 l3)
           const uint32_t a = w[half][2 * g], c = w[half][2 * g + 1];
@@ -322,33 +338,15 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     STAMP(2);
     __syncthreads();
     STAMP(3);
-    // phase-5 operands requested now, consumed after the transform (latency
-    // hidden behind it): the E[y] multiply tables of this lane's erased output
-    // rows y = 4 lane + q and the 8 bytes of its present ones
+    // phase-5 tables requested now, consumed after the transform (latency
+    // hidden behind it): E[y] of this lane's erased output rows y = 4 lane + q
+    // (its present ones are in the staging area)
     const uint64_t cbase = col0 + 4 * wave;
-    const bool whole = cbase + 4 <= ncols;
     Tab T5[4];
-    uint32_t ra[4], rc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const uint32_t y = 4 * lane + q;
       const uint32_t m = (meta[2 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
-      ra[q] = rc[q] = 0;
-      if (m != 0xFFFFu) {
-        load_tab(t.mtab, m, T5[q]);
-      } else {
-        const uint8_t *row = SH + uint64_t(y) * sstride + 2 * cbase;
-        if (whole) {
-          const uint2 d = *reinterpret_cast<const uint2 *>(row);
-          ra[q] = d.x;
-          rc[q] = d.y;
-        } else {
-          for (uint64_t e = 0; e < 2 * (ncols > cbase ? ncols - cbase : 0); ++e) {
-            if (e < 4) ra[q] |= uint32_t(row[e]) << (8 * e);
-            else rc[q] |= uint32_t(row[e]) << (8 * (e - 4));
-          }
-        }
-      }
+      if (m != 0xFFFFu) load_tab(t.mtab, m, T5[q]);
     }
 
     // ---- phase 2: IFFT_1024 on this wave's group
@@ -554,6 +552,18 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     // reconstructSub:138-149).  No workgroup barrier: the operands were
     // requested before the transform.
     {
+      uint32_t ra[4], rc[4];  // rows 4 lane .. + 3, group `wave`, as received
+      {
+        uint32_t ol2 = lane;
+        asm volatile("" : "+v"(ol2));
+        const uint32_t sa = lds_addr(stage) + stage_addr(4 * ol2, wave);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint2 d = lds_ld2(sa + 8 * q);
+          ra[q] = d.x;
+          rc[q] = d.y;
+        }
+      }
       uint32_t ol[4], oh[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
