@@ -9,9 +9,12 @@ are in KiB summed over the TCC instances.  FETCH_SIZE reports half the bytes of
 reconstruct kernel's 64-B-per-lane row reads (/1.043).  WRITE_SIZE is exact for
 the 16-B-per-lane stores.
   encode:       fetch = raw x 2 (payload reads are 16 B per lane)
-  reconstruct:  fetch = (raw - p5/2) / 1.043 + p5, where p5 = the phase-5
-                8-B-per-lane re-reads of present data rows y < k, known exactly
-                from the workload: B x (present rows < k) x shard_len.
+  reconstruct:  fetch = raw / 1.043.  (Until r02 the kernel re-read the
+                present data rows y < k in phase 5, 8 B per lane, and this
+                added them back as p5 = B x (present rows < k) x shard_len at
+                half weight.  Since r02 those rows are staged in LDS; the raw
+                count did not move when the re-read went away (7.01 vs 7.00
+                GB), i.e. the re-reads had been L2 hits, not HBM traffic.)
 usage: pmc_summary.py SRC DST B NV PAYLOAD PRESENT
 """
 import csv
@@ -47,7 +50,7 @@ def per_launch(path, counter):
 
 fetch = per_launch(f"{src}/FETCH_SIZE/run_counter_collection.csv", "FETCH_SIZE")
 write = per_launch(f"{src}/WRITE_SIZE/run_counter_collection.csv", "WRITE_SIZE")
-p5 = B * (CNT * K / N) * SL  # expected phase-5 re-read bytes (present rows < k)
+p5 = 0  # phase-5 re-reads: none since r02 (LDS staging)
 res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, kernel-trace only",
        "workload": {"batch": B, "n_validators": NV, "payload_bytes": P, "present": CNT,
                     "shard_len": SL},
