@@ -53,7 +53,7 @@ __host__ __device__ constexpr uint32_t tlin(uint32_t idx) {
 
 __device__ __forceinline__ void lds_tab_at(const uint8_t *lds, uint32_t lin, Tab &T) {
 #pragma unroll
-  for (int q = 0; q < 5; ++q) {
+  for (int q = 4; q >= 0; --q) {  // plane 0 (first used) last: one wait per table
     const uint4 v = *reinterpret_cast<const uint4 *>(lds + q * Tabs::kPlane + lin);
     T.t[4 * q] = v.x;
     T.t[4 * q + 1] = v.y;
