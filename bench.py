@@ -111,7 +111,8 @@ def cpu_baseline(nv, plen, cnt, seconds):
     return res
 
 
-def scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out, step_s, timeout_s):
+def scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out, step_s, timeout_s,
+                   on_timeout=None):
     """SURVEY.md §8e / north_star: the batch starts on GPU0 and the decoded
     payloads end there.  Rank 0 holds every rank's payloads, scatters them over
     RCCL (one grouped batch of ncclSend / ncclRecv: each rank's slice on its own
@@ -125,9 +126,18 @@ def scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out, step_s, timeou
     def watchdog():  # a hung collective must not cost the main measurement
         if not done.wait(timeout_s):
             print(json.dumps({"scatter_gather_timeout_s": timeout_s}), file=sys.stderr, flush=True)
-            os._exit(3)
+            if on_timeout:
+                on_timeout()  # rank 0: the measurement line, marked
+            os._exit(0)
 
     threading.Thread(target=watchdog, daemon=True).start()
+    try:
+        return _scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out, step_s)
+    finally:
+        done.set()
+
+
+def _scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out, step_s):
     whole = None
     if rank == 0:
         whole = torch.empty((world, B, plen), dtype=torch.uint8, device=dev)
@@ -164,7 +174,6 @@ def scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out, step_s, timeou
         del gath, whole
     flag = torch.tensor([ok], dtype=torch.int32, device=dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    done.set()
     sc_bytes = (world - 1) * B * plen
     ga_bytes = (world - 1) * B * ob
     return {"scatter_ms": round(t_sc * 1e3, 3), "scatter_bytes": sc_bytes,
@@ -297,14 +306,26 @@ def main():
         "reconstruct_GiBps": round(world * B * plen / ((t_loc + t_rec) * 1e-3) / 2**30, 3),
         "roundtrip_ok": ok,
     }
+    if rank == 0 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(nv, plen, cnt, args.cpu_seconds)
+    sg_failed = False
     if dist and backend == "nccl" and not args.no_scatter:
-        line["scatter_gather"] = scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out,
-                                                elapsed / args.steps, args.scatter_timeout)
+        # the device-resident line above is the measurement; the scatter /
+        # gather is reported beside it and can neither hang nor fail it
+        def on_timeout():
+            if rank == 0:
+                line["scatter_gather"] = {"timeout_s": args.scatter_timeout}
+                print(json.dumps(line), flush=True)
+        try:
+            line["scatter_gather"] = scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out,
+                                                    elapsed / args.steps, args.scatter_timeout,
+                                                    on_timeout)
+        except Exception as exc:  # noqa: BLE001 (reported, not raised)
+            sg_failed = True
+            line["scatter_gather"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
     if rank == 0:
-        if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(nv, plen, cnt, args.cpu_seconds)
         print(json.dumps(line), flush=True)
-    if dist:
+    if dist and not sg_failed:
         dist.destroy_process_group()
     if not ok:
         sys.exit(1)
