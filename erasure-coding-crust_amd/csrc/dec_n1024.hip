@@ -187,13 +187,15 @@ __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ?
 }  // namespace
 
 // Gather order of a payload's 1024 received rows (its erasure pattern): the
-// present rows first, then the absent ones, dealt round-robin over the 8
-// waves (slot s of each half -> wave s % 8, lane s / 8), stored in the order
-// threads read it: entry [half * 512 + tid] = (row << 16) | mul_index(E[row])
-// for a present row, (row << 16) | 0xFFFF for an absent one.  A wave whose
-// slots of a half are all absent then skips that half's multiplies (uniform
-// branch); with 1/3 of the rows present (threshold) that is every wave's
-// second half, where the natural row order multiplied in every wave.
+// present rows first, then the absent ones, dealt wave-major (slot s of each
+// half -> wave s / 64, lane s % 64; waves w and w + 4 share a SIMD), stored in
+// the order threads read it: entry [half * 512 + tid] = (row << 16) |
+// mul_index(E[row]) for a present row, (row << 16) | 0xFFFF for an absent
+// one.  A wave whose slots of a half are all absent skips that half's
+// multiplies (uniform branch): with 342 of 1024 rows present (threshold) every
+// second half and waves 6, 7 of the first; with k = 256 present also waves
+// 4, 5, so no SIMD multiplies more than one wave's rows (the natural row
+// order multiplied in every wave and half).
 __global__ void __launch_bounds__(1024) n1024_order(const uint8_t *__restrict__ present,
                                                     const uint16_t *__restrict__ elog,
                                                     const uint32_t *__restrict__ pattern, int nv,
@@ -215,7 +217,7 @@ __global__ void __launch_bounds__(1024) n1024_order(const uint8_t *__restrict__ 
   // slot: present rows in row order, then absent rows in row order
   const uint32_t slot = f ? pw + below : c + (64 * w - pw) + (lane - below);
   const uint32_t half = slot >> 9, sp = slot & 511;
-  const uint32_t t = (sp & 7) * 64 + (sp >> 3);
+  const uint32_t t = sp;  // wave-major: slot s -> wave s / 64 (on SIMD (s / 64) % 4)
   order[uint64_t(b) * N + half * 512 + t] = (v << 16) | (f ? mul_index(elog[pt * N + v]) : 0xFFFFu);
 }
 
