@@ -186,24 +186,26 @@ __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ?
 
 }  // namespace
 
-// Gather order of a payload's 1024 received rows (its erasure pattern): the
-// present rows first, then the absent ones, dealt wave-major (slot s of each
-// half -> wave s / 64, lane s % 64; waves w and w + 4 share a SIMD), stored in
-// the order threads read it: entry [half * 512 + tid] = (row << 16) |
-// mul_index(E[row]) for a present row, (row << 16) | 0xFFFF for an absent
-// one.  A wave whose slots of a half are all absent skips that half's
-// multiplies (uniform branch): with 342 of 1024 rows present (threshold) every
-// second half and waves 6, 7 of the first; with k = 256 present also waves
-// 4, 5, so no SIMD multiplies more than one wave's rows (the natural row
-// order multiplied in every wave and half).
-__global__ void __launch_bounds__(1024) n1024_order(const uint8_t *__restrict__ present,
-                                                    const uint16_t *__restrict__ elog,
-                                                    const uint32_t *__restrict__ pattern, int nv,
-                                                    uint32_t *__restrict__ order) {
+// Gather order of a payload's received rows (its erasure pattern), per
+// 1024-row quarter (n = 1024: one; reconstruct_n4096: n / 1024): the present
+// rows first, then the absent ones, dealt wave-major (slot s of each half ->
+// wave s / 64, lane s % 64; waves w and w + 4 share a SIMD), stored in the
+// order threads read it: entry [(b * Q + q) * 1024 + half * 512 + tid] =
+// (row in quarter << 16) | mul_index(E[row]) for a present row, | 0xFFFF for
+// an absent one.  A wave whose slots of a half are all absent skips that
+// half's multiplies (uniform branch): with 342 of 1024 rows present
+// (threshold) every second half and waves 6, 7 of the first; with k = 256
+// present also waves 4, 5, so no SIMD multiplies more than one wave's rows
+// (the natural row order multiplied in every wave and half).
+__global__ void __launch_bounds__(1024) gather_order(const uint8_t *__restrict__ present,
+                                                     const uint16_t *__restrict__ elog,
+                                                     const uint32_t *__restrict__ pattern, int nv,
+                                                     uint32_t nq, uint32_t *__restrict__ order) {
   __shared__ uint32_t cnt[16];
-  const uint32_t b = blockIdx.x, v = threadIdx.x, lane = v & 63, w = v >> 6;
-  const uint64_t pt = pattern ? pattern[b] : b;
-  const bool f = int(v) < nv && present[pt * N + v] != 0;
+  const uint32_t b = blockIdx.x / nq, q = blockIdx.x % nq;
+  const uint32_t v = threadIdx.x, lane = v & 63, w = v >> 6, row = 1024 * q + v;
+  const uint64_t n = 1024ull * nq, pt = pattern ? pattern[b] : b;
+  const bool f = int(row) < nv && present[pt * n + row] != 0;
   const uint64_t m = __ballot(f);
   const uint32_t below = __popcll(m & ((1ull << lane) - 1));
   if (lane == 0) cnt[w] = uint32_t(__popcll(m));
@@ -214,12 +216,24 @@ __global__ void __launch_bounds__(1024) n1024_order(const uint8_t *__restrict__ 
     pw += i < int(w) ? cnt[i] : 0u;
     c += cnt[i];
   }
-  // slot: present rows in row order, then absent rows in row order
+  // slot: present rows in row order, then absent rows in row order; slot s
+  // of the quarter is read by thread s % 512 in half s / 512
   const uint32_t slot = f ? pw + below : c + (64 * w - pw) + (lane - below);
-  const uint32_t half = slot >> 9, sp = slot & 511;
-  const uint32_t t = sp;  // wave-major: slot s -> wave s / 64 (on SIMD (s / 64) % 4)
-  order[uint64_t(b) * N + half * 512 + t] = (v << 16) | (f ? mul_index(elog[pt * N + v]) : 0xFFFFu);
+  order[uint64_t(blockIdx.x) * 1024 + slot] =
+      (v << 16) | (f ? mul_index(elog[pt * n + row]) : 0xFFFFu);
 }
+
+hipError_t launch_gather_order(const CodeParams &p, const uint8_t *d_present,
+                               const uint16_t *d_err_log, const uint32_t *d_pattern, size_t batch,
+                               uint32_t *order, hipStream_t s) {
+  if (p.n % 1024 != 0) return hipErrorInvalidValue;
+  const uint32_t nq = p.n / 1024;
+  hipLaunchKernelGGL(gather_order, dim3(unsigned(batch * nq)), dim3(1024), 0, s, d_present, d_err_log,
+                     d_pattern, int(p.nv), nq, order);
+  return hipGetLastError();
+}
+
+size_t gather_order_bytes(const CodeParams &p, size_t batch) { return batch * p.n * sizeof(uint32_t); }
 
 __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
@@ -242,7 +256,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   const uint64_t ncols = slen / 2;
   const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);
   const uint64_t total = uint64_t(tiles_pp) * batch;
-  // m[0], m[1]: this thread's two gather slots (n1024_order): row << 16 |
+  // m[0], m[1]: this thread's two gather slots (gather_order): row << 16 |
   // mul_index(E[row]), low half 0xFFFF = absent.  Loaded one tile ahead so the
   // gather's table loads wait on one global latency instead of two.
   // m[2], m[3]: the output rows y = 4 lane + q (q = 0..3) of phase 5, 16 bits
@@ -278,7 +292,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     uint8_t *O = out + b * ostride;
 
     // ---- phase 1: gather + scale this thread's two slots' rows (present rows
-    // first, n1024_order; decode_main:174-177); absent rows are written as 0.
+    // first, gather_order; decode_main:174-177); absent rows are written as 0.
     // The first slot's row and E[v] table are requested before the barrier
     // (they only land in registers), so their latency overlaps the wait for
     // the other waves' previous tile; the second slot (mostly absent rows:
@@ -614,9 +628,10 @@ hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
       e != hipSuccess)
     return e;
   if (!scratch) return hipErrorInvalidValue;
-  uint32_t *order = static_cast<uint32_t *>(scratch);  // n1024_scratch_bytes(batch)
-  hipLaunchKernelGGL(n1024_order, dim3(unsigned(batch)), dim3(1024), 0, s, d_present, d_err_log,
-                     d_pattern, int(p.nv), order);
+  uint32_t *order = static_cast<uint32_t *>(scratch);  // gather_order_bytes(p, batch)
+  if (const hipError_t e = launch_gather_order(p, d_present, d_err_log, d_pattern, batch, order, s);
+      e != hipSuccess)
+    return e;
   const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   hipLaunchKernelGGL(reconstruct_n1024, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
@@ -625,6 +640,5 @@ hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
   return hipGetLastError();
 }
 
-size_t n1024_scratch_bytes(size_t batch) { return batch * N * sizeof(uint32_t); }
 
 }  // namespace ecamd

@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(THREADS)
 reconstruct_n4096(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
-    const uint32_t *__restrict__ pattern,
+    const uint32_t *__restrict__ pattern, const uint32_t *__restrict__ order,
     uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t K, uint32_t batch,
     DevTables t, Lin lin) {
   constexpr int N = 1024 * NQ;
@@ -109,19 +109,18 @@ reconstruct_n4096(
     const uint16_t *E = elog + pt * N;
     uint8_t *O = out + b * ostride;
     S16 P, Qa;  // the two accumulators of the linearised cross-quarter stages
-    // gather-row metadata of a quarter (rows 1024q + tid, + 512): bit 16 = present
-    // (and < nv), bits 0-15 = mul_index(E[v]).  The next quarter's is loaded
-    // right after a quarter's gather, so its gather waits on one global latency
-    // (the table and the row) instead of two (present/E first).
+    // this thread's two gather slots of a quarter (gather_order, dec_n1024.hip:
+    // present rows first, dealt wave-major): (row in quarter << 16) |
+    // mul_index(E[row]), low half 0xFFFF = absent.  The next quarter's are
+    // loaded right after a quarter's gather, so its gather waits on one global
+    // latency (the table and the row) instead of two.
     uint32_t mq[1024 / THREADS];
     const auto load_meta = [&](const int q, const uint32_t tq) __attribute__((always_inline)) {
 #pragma unroll
-      for (int half = 0; half < 1024 / THREADS; ++half) {
-        const uint32_t v = 1024 * q + tq + half * THREADS;
-        const uint32_t pv = pr[v], ev = E[v];
-        mq[half] = mul_index(ev) | ((pv != 0 && int(v) < nv) ? 0x10000u : 0u);
-      }
+      for (int half = 0; half < 1024 / THREADS; ++half)
+        mq[half] = order[(b * NQ + q) * 1024 + half * THREADS + tq];
     };
+    const auto has = [&](int half) { return (mq[half] & 0xffffu) != 0xffffu; };
 
     // ---- IFFT quarters 3, 2, 1, 0 (quarter 0's tables stay for the FFT), each
     // folded into P and Qa as soon as it is transformed
@@ -139,7 +138,7 @@ reconstruct_n4096(
       Tab RT[1024 / THREADS];
       const uint64_t avail = slen - 2 * col0;
       const auto load_row = [&](int half) __attribute__((always_inline)) {
-        const uint8_t *row = SH + uint64_t(1024 * q + tq + half * THREADS) * sstride + 2 * col0;
+        const uint8_t *row = SH + uint64_t(1024 * q + (mq[half] >> 16)) * sstride + 2 * col0;
         if (avail >= 64) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -154,7 +153,7 @@ reconstruct_n4096(
         }
         load_tab(t.mtab, mq[half] & 0xffffu, RT[half]);
       };
-      if (mq[0] & 0x10000u) load_row(0);
+      if (has(0)) load_row(0);
       lds_barrier();  // every wave is done with the tables and its region
       // the quarter's tables (skews 1024q + i) by LDS-DMA, in the background
       // of the row gather; retired before the barrier below
@@ -162,11 +161,11 @@ reconstruct_n4096(
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int half = 0; half < 1024 / THREADS; ++half) {
-        const uint32_t vl = tq + half * THREADS;
+        const uint32_t vl = mq[half] >> 16;
         uint32_t l[8], h[8];
 #pragma unroll
         for (int g = 0; g < 8; ++g) l[g] = h[g] = 0;
-        if (mq[half] & 0x10000u) {
+        if (has(half)) {
           if (half > 0) load_row(half);
 #pragma unroll
           for (int g = 0; g < 8; ++g) {
@@ -373,7 +372,8 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
                                     const uint8_t *d_shards, size_t slen, size_t sstride,
                                     const uint8_t *d_present, const uint16_t *d_err_log,
                                     const uint32_t *d_pattern,
-                                    size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
+                                    size_t batch, uint8_t *d_out, size_t ostride, void *scratch,
+                                    hipStream_t s) {
   int cus = 0;
   const void *fn = nullptr;
   if (p.n == 4096) fn = p.k == 1024 ? reinterpret_cast<const void *>(&reconstruct_n4096<4, 10>)
@@ -381,13 +381,18 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
   else fn = p.k == 512 ? reinterpret_cast<const void *>(&reconstruct_n4096<2, 9>)
                        : reinterpret_cast<const void *>(&reconstruct_n4096<2, 8>);
   if (const hipError_t e = prepare_kernel(fn, LDS_BYTES, &cus); e != hipSuccess) return e;
+  if (!scratch) return hipErrorInvalidValue;
+  uint32_t *order = static_cast<uint32_t *>(scratch);  // gather_order_bytes(p, batch)
+  if (const hipError_t e = launch_gather_order(p, d_present, d_err_log, d_pattern, batch, order, s);
+      e != hipSuccess)
+    return e;
   const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   static const Lin lin4 = n4096_lin(4), lin2 = n4096_lin(2);
 #define ECAMD_D4(NQv, KBv)                                                                    \
   if (p.n == 1024u * NQv && p.k == (1u << KBv))                                                  \
     hipLaunchKernelGGL((reconstruct_n4096<NQv, KBv>), dim3(grid), dim3(THREADS), LDS_BYTES, s,   \
-                       d_shards, uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, d_out, \
+                       d_shards, uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, order, d_out, \
                        uint64_t(ostride), int(p.nv), uint32_t(p.k), uint32_t(batch), t,         \
                        NQv == 4 ? lin4 : lin2);
   ECAMD_D4(4, 10)

@@ -484,7 +484,7 @@ hipError_t launch_broadcast_locators(const CodeParams &p, const uint32_t *d_patt
 }
 
 size_t reconstruct_scratch_bytes(const CodeParams &p, size_t slen, size_t batch) {
-  if (n1024_applicable(p)) return n1024_scratch_bytes(batch);
+  if (n1024_applicable(p) || n4096_applicable(p)) return gather_order_bytes(p, batch);
   if (p.n <= uint32_t(kLdsSlots)) return 0;
   const size_t tiles = (slen / 2 + 3) / 4;
   return tiles * grid_y(batch) * 2 * size_t(p.n) * sizeof(uint2);
@@ -504,7 +504,7 @@ hipError_t launch_reconstruct(const CodeParams &p, const DevTables &t, const uin
   if (aligned && n4096_applicable(p) && reinterpret_cast<uintptr_t>(d_out) % 16 == 0 &&
       (batch == 1 || ostride % 16 == 0))
     return launch_reconstruct_n4096(p, t, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch,
-                                    d_out, ostride, s);
+                                    d_out, ostride, scratch, s);
   if (aligned && decgen_applicable(p) && reinterpret_cast<uintptr_t>(d_out) % 16 == 0 &&
       (batch == 1 || ostride % 16 == 0))
     return launch_reconstruct_gen(p, t, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch,

@@ -37,7 +37,7 @@ int main() {
   (void)hipMemcpy(dp, pres.data(), pres.size(), hipMemcpyHostToDevice);
   (void)hipMemcpy(de, el.data(), el.size() * 2, hipMemcpyHostToDevice);
   void *order = nullptr;
-  (void)hipMalloc(&order, n1024_scratch_bytes(B));
+  (void)hipMalloc(&order, gather_order_bytes(p, B));
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
