@@ -90,7 +90,7 @@ template <int L, int KB>
 __global__ void __launch_bounds__(THREADS) reconstruct_gen(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
-    const uint32_t *__restrict__ pattern,
+    const uint32_t *__restrict__ pattern, const uint32_t *__restrict__ order,
     uint8_t *__restrict__ out, uint64_t ostride, int nv, int k, uint32_t batch, DevTables t) {
   constexpr int N = 1 << L;
   constexpr uint32_t NM = N - 1;
@@ -120,8 +120,13 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
   const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
   const uint64_t tile_end = per * (blockIdx.x + 1) < total ? per * (blockIdx.x + 1) : total;
   uint64_t cur_b = ~0ull;
+  // this thread's received rows: slot rr * THREADS + tid (RPT = 2) or
+  // tid * CPT / CPR (several threads per row) of the payload's gather order
+  // (gather_order: present rows first, wave-major), so a wave whose rows are
+  // all absent skips the gather's multiplies
   Tab RT[RPT];  // E[v] tables of this thread's received rows
   bool rhave[RPT];
+  uint32_t rv[RPT];
   // the next tile's received rows are requested at the end of each gather and
   // land during the transform (same payload and a whole tile only)
   uint4 pre[CPT];
@@ -143,9 +148,11 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
       cur_b = b;
 #pragma unroll
       for (int rr = 0; rr < RPT; ++rr) {
-        const uint32_t v = (tid * CPT + rr * JPR) / CPR;
-        rhave[rr] = int(v) < nv && pr[v];
-        load_tab(t.mtab, mul_index(E[v]), RT[rr]);  // absent rows: any table times zero
+        const uint32_t slot = RPT == 2 ? rr * THREADS + tid : tid * CPT / CPR;
+        const uint32_t e = order[b * N + slot];
+        rv[rr] = e >> 16;
+        rhave[rr] = (e & 0xffffu) != 0xffffu;
+        load_tab(t.mtab, rhave[rr] ? (e & 0xffffu) : 0u, RT[rr]);
       }
 #pragma unroll
       for (int it = 0; it < (128 * 5 + THREADS - 1) / THREADS; ++it) {  // k * 5 <= 640 chunks
@@ -162,12 +169,13 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
       const uint64_t avail = slen - 2 * col0;  // bytes of a row inside the tile
 #pragma unroll
       for (int rr = 0; rr < RPT; ++rr) {
-        const uint32_t ch0 = tid * CPT + rr * JPR, v = ch0 / CPR;
+        const uint32_t cr = RPT == 2 ? 0u : (tid * CPT) % CPR;  // first chunk of the row
+        const uint32_t v = rv[rr];
         const bool have = rhave[rr];
         const Tab &T = RT[rr];
 #pragma unroll
         for (int j = 0; j < JPR; ++j) {
-          const uint32_t c16 = ch0 % CPR + j;
+          const uint32_t c16 = cr + j;
           uint32_t w[4] = {0, 0, 0, 0};
           if (have && pre_ok) {
             const uint4 d = pre[rr * JPR + j];
@@ -186,8 +194,10 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
           for (int h2 = 0; h2 < 2; ++h2) {  // columns 8 c16 + 4 h2 .. + 3 = group 2 c16 + h2
             const uint32_t g = 2 * c16 + h2, gw = g / INST, gi = g % INST;
             uint32_t l = 0, h = 0;
-            const uint32_t a = w[2 * h2], c = w[2 * h2 + 1];
-            mul_acc(vperm(c, a, 0x07050301u), vperm(c, a, 0x06040200u), T, l, h);
+            if (have) {  // a wave with no present row skips (exec mask empty)
+              const uint32_t a = w[2 * h2], c = w[2 * h2 + 1];
+              mul_acc(vperm(c, a, 0x07050301u), vperm(c, a, 0x06040200u), T, l, h);
+            }
             *reinterpret_cast<uint2 *>(regions + gw * REG_BYTES + raddr((gi << L) | v)) =
                 make_uint2(l, h);
           }
@@ -199,12 +209,12 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
       if (pre_ok) {
 #pragma unroll
         for (int rr = 0; rr < RPT; ++rr) {
-          const uint32_t ch0 = tid * CPT + rr * JPR, v = ch0 / CPR;
+          const uint32_t cr = RPT == 2 ? 0u : (tid * CPT) % CPR;
           if (!rhave[rr]) continue;
 #pragma unroll
           for (int j = 0; j < JPR; ++j)
             pre[rr * JPR + j] = *reinterpret_cast<const uint4 *>(
-                SH + uint64_t(v) * sstride + 2 * ncol0 + 16 * (ch0 % CPR + j));
+                SH + uint64_t(rv[rr]) * sstride + 2 * ncol0 + 16 * (cr + j));
         }
       }
     }
@@ -320,7 +330,7 @@ template <int L, int KB>
 hipError_t launch_l(const CodeParams &p, const DevTables &t, const uint8_t *d_shards, size_t slen,
                     size_t sstride, const uint8_t *d_present, const uint16_t *d_err_log,
                                     const uint32_t *d_pattern,
-                    size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
+                    size_t batch, uint8_t *d_out, size_t ostride, const uint32_t *order, hipStream_t s) {
   int cus = 0;
   if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&reconstruct_gen<L, KB>),
                                           LDS_BYTES, &cus);
@@ -330,7 +340,7 @@ hipError_t launch_l(const CodeParams &p, const DevTables &t, const uint8_t *d_sh
   const size_t tiles = (slen / 2 + TC - 1) / TC * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   hipLaunchKernelGGL((reconstruct_gen<L, KB>), dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
-                     uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, d_out,
+                     uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, order, d_out,
                      uint64_t(ostride), int(p.nv), int(p.k), uint32_t(batch), t);
   return hipGetLastError();
 }
@@ -346,12 +356,18 @@ bool decgen_applicable(const CodeParams &p) {  // the (n, k) instantiated below
 hipError_t launch_reconstruct_gen(const CodeParams &p, const DevTables &t,
                                   const uint8_t *d_shards, size_t slen, size_t sstride,
                                   const uint8_t *d_present, const uint16_t *d_err_log,
-                                    const uint32_t *d_pattern,
-                                  size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s) {
+                                  const uint32_t *d_pattern,
+                                  size_t batch, uint8_t *d_out, size_t ostride, void *scratch,
+                                  hipStream_t s) {
+  if (!scratch) return hipErrorInvalidValue;
+  uint32_t *order = static_cast<uint32_t *>(scratch);  // gather_order_bytes(p, batch)
+  if (const hipError_t e = launch_gather_order(p, d_present, d_err_log, d_pattern, batch, order, s);
+      e != hipSuccess)
+    return e;
 #define ECAMD_DG(Lv, KBv)                                                                   \
   if (p.n == (1u << Lv) && p.k == (1u << KBv))                                             \
     return launch_l<Lv, KBv>(p, t, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch, d_out, \
-                             ostride, s);
+                             ostride, order, s);
   // every (n, k) of 46 <= n_validators <= 765 (decgen_applicable)
   ECAMD_DG(6, 4)
   ECAMD_DG(7, 4)

@@ -187,7 +187,8 @@ __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ?
 }  // namespace
 
 // Gather order of a payload's received rows (its erasure pattern), per
-// 1024-row quarter (n = 1024: one; reconstruct_n4096: n / 1024): the present
+// 1024-row quarter (n = 1024: one; reconstruct_n4096: n / 1024; n < 1024:
+// the n rows, reconstruct_gen): the present
 // rows first, then the absent ones, dealt wave-major (slot s of each half ->
 // wave s / 64, lane s % 64; waves w and w + 4 share a SIMD), stored in the
 // order threads read it: entry [(b * Q + q) * 1024 + half * 512 + tid] =
@@ -200,12 +201,15 @@ __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ?
 __global__ void __launch_bounds__(1024) gather_order(const uint8_t *__restrict__ present,
                                                      const uint16_t *__restrict__ elog,
                                                      const uint32_t *__restrict__ pattern, int nv,
-                                                     uint32_t nq, uint32_t *__restrict__ order) {
+                                                     uint32_t n, uint32_t rows, uint32_t nq,
+                                                     uint32_t *__restrict__ order) {
   __shared__ uint32_t cnt[16];
   const uint32_t b = blockIdx.x / nq, q = blockIdx.x % nq;
   const uint32_t v = threadIdx.x, lane = v & 63, w = v >> 6, row = 1024 * q + v;
-  const uint64_t n = 1024ull * nq, pt = pattern ? pattern[b] : b;
-  const bool f = int(row) < nv && present[pt * n + row] != 0;
+  const uint64_t pt = pattern ? pattern[b] : b;
+  // rows of the block: 1024, or n < 1024 (threads v >= n are absent and, being
+  // last in thread order, take slots >= n, which are not written)
+  const bool f = v < rows && int(row) < nv && present[pt * n + row] != 0;
   const uint64_t m = __ballot(f);
   const uint32_t below = __popcll(m & ((1ull << lane) - 1));
   if (lane == 0) cnt[w] = uint32_t(__popcll(m));
@@ -219,17 +223,17 @@ __global__ void __launch_bounds__(1024) gather_order(const uint8_t *__restrict__
   // slot: present rows in row order, then absent rows in row order; slot s
   // of the quarter is read by thread s % 512 in half s / 512
   const uint32_t slot = f ? pw + below : c + (64 * w - pw) + (lane - below);
-  order[uint64_t(blockIdx.x) * 1024 + slot] =
-      (v << 16) | (f ? mul_index(elog[pt * n + row]) : 0xFFFFu);
+  if (v < rows)
+    order[uint64_t(b) * n + 1024 * q + slot] = (v << 16) | (f ? mul_index(elog[pt * n + row]) : 0xFFFFu);
 }
 
 hipError_t launch_gather_order(const CodeParams &p, const uint8_t *d_present,
                                const uint16_t *d_err_log, const uint32_t *d_pattern, size_t batch,
                                uint32_t *order, hipStream_t s) {
-  if (p.n % 1024 != 0) return hipErrorInvalidValue;
-  const uint32_t nq = p.n / 1024;
+  if (p.n > 1024 && p.n % 1024 != 0) return hipErrorInvalidValue;
+  const uint32_t rows = p.n < 1024 ? p.n : 1024, nq = p.n / rows;
   hipLaunchKernelGGL(gather_order, dim3(unsigned(batch * nq)), dim3(1024), 0, s, d_present, d_err_log,
-                     d_pattern, int(p.nv), nq, order);
+                     d_pattern, int(p.nv), uint32_t(p.n), rows, nq, order);
   return hipGetLastError();
 }
 

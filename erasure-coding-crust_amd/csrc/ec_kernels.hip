@@ -484,7 +484,8 @@ hipError_t launch_broadcast_locators(const CodeParams &p, const uint32_t *d_patt
 }
 
 size_t reconstruct_scratch_bytes(const CodeParams &p, size_t slen, size_t batch) {
-  if (n1024_applicable(p) || n4096_applicable(p)) return gather_order_bytes(p, batch);
+  if (n1024_applicable(p) || n4096_applicable(p) || decgen_applicable(p))
+    return gather_order_bytes(p, batch);
   if (p.n <= uint32_t(kLdsSlots)) return 0;
   const size_t tiles = (slen / 2 + 3) / 4;
   return tiles * grid_y(batch) * 2 * size_t(p.n) * sizeof(uint2);
@@ -508,7 +509,7 @@ hipError_t launch_reconstruct(const CodeParams &p, const DevTables &t, const uin
   if (aligned && decgen_applicable(p) && reinterpret_cast<uintptr_t>(d_out) % 16 == 0 &&
       (batch == 1 || ostride % 16 == 0))
     return launch_reconstruct_gen(p, t, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch,
-                                  d_out, ostride, s);
+                                  d_out, ostride, scratch, s);
   const int G = groups_for(p.n);
   const size_t tiles = (slen / 2 + 4 * G - 1) / (4 * G);
   const bool lds = p.n <= uint32_t(kLdsSlots);

@@ -86,8 +86,8 @@ hipError_t launch_encode_gen(const CodeParams &p, const DevTables &t, const uint
                              size_t sstride, hipStream_t s);
 
 // Per-payload gather order of the received rows, present rows first, per
-// 1024-row quarter (n a multiple of 1024; dec_n1024.hip): the scratch of
-// reconstruct_n1024 and reconstruct_n4096, gather_order_bytes(p, batch)
+// 1024-row quarter (or the n < 1024 rows; dec_n1024.hip): the scratch of
+// reconstruct_n1024, _n4096 and _gen, gather_order_bytes(p, batch)
 size_t gather_order_bytes(const CodeParams &p, size_t batch);
 hipError_t launch_gather_order(const CodeParams &p, const uint8_t *d_present,
                                const uint16_t *d_err_log, const uint32_t *d_pattern, size_t batch,
@@ -109,11 +109,13 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
                                     const uint32_t *d_pattern, size_t batch, uint8_t *d_out,
                                     size_t ostride, void *scratch, hipStream_t s);
 
-// register-blocked reconstruct for 64 <= n <= 1024, 16 <= k <= 512 (dec_gen.hip)
+// register-blocked reconstruct for 64 <= n <= 1024, 16 <= k <= 512 (dec_gen.hip);
+// scratch: gather_order_bytes(p, batch)
 bool decgen_applicable(const CodeParams &p);
 hipError_t launch_reconstruct_gen(const CodeParams &p, const DevTables &t,
                                   const uint8_t *d_shards, size_t slen, size_t sstride,
                                   const uint8_t *d_present, const uint16_t *d_err_log,
-                                  const uint32_t *d_pattern, size_t batch, uint8_t *d_out, size_t ostride, hipStream_t s);
+                                  const uint32_t *d_pattern, size_t batch, uint8_t *d_out,
+                                  size_t ostride, void *scratch, hipStream_t s);
 
 }  // namespace ecamd
