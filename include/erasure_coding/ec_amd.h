@@ -6,7 +6,8 @@
  * is a hipStream_t (NULL = the legacy default stream).  Calls are asynchronous
  * on `stream` and the caller owns every buffer it passes.  They are NOT
  * graph-capture-safe in general: the first call per (device, kernel) sets a
- * kernel attribute; shapes that need device scratch (k = 1024 encodes, n > 4096
+ * kernel attribute; shapes that need device scratch (k = 1024 encodes, the
+ * fast reconstructs' per-payload gather order (4 n bytes per payload), n > 4096
  * generic kernels, ECCR_AMD_error_locator / ECCR_AMD_dedup_patterns with
  * batch > 1) take a per-device scratch buffer that may be (re)allocated with
  * hipMalloc / hipFree and is ordered across streams with an event
