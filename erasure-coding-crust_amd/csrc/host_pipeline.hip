@@ -55,7 +55,12 @@ struct Slot {
   uint8_t *d_a = nullptr, *d_b = nullptr, *d_c = nullptr, *d_present = nullptr;
   uint16_t *d_elog = nullptr, *d_idx = nullptr;
   uint32_t *d_pat = nullptr;
-  size_t cap_a = 0, cap_b = 0, cap_c = 0, cap_present = 0, cap_elog = 0, cap_idx = 0, cap_pat = 0;
+  // the slot's own kernel scratch (k = 1024 encode coefficients, reconstruct
+  // gather orders): stream-ordered by the slot, so the three slots overlap; a
+  // shared per-device lease would order them behind each other
+  uint8_t *d_scr = nullptr;
+  size_t cap_a = 0, cap_b = 0, cap_c = 0, cap_present = 0, cap_elog = 0, cap_idx = 0, cap_pat = 0,
+         cap_scr = 0;
   // host staging of a chunk's distinct erasure patterns; `staged` is recorded
   // after their upload so the next chunk on this slot does not overwrite them early
   std::vector<uint8_t> h_rows;
@@ -81,7 +86,8 @@ struct Pipeline {
       if (s.staged) (void)hipEventDestroy(s.staged);
       for (void *p : {static_cast<void *>(s.d_a), static_cast<void *>(s.d_b), static_cast<void *>(s.d_c),
                       static_cast<void *>(s.d_present), static_cast<void *>(s.d_elog),
-                      static_cast<void *>(s.d_idx), static_cast<void *>(s.d_pat)})
+                      static_cast<void *>(s.d_idx), static_cast<void *>(s.d_pat),
+                      static_cast<void *>(s.d_scr)})
         if (p) (void)hipFree(p);
       s = Slot{};
     }
@@ -122,6 +128,15 @@ Pipeline *pipeline() {  // one per host thread (reentrant like the reference)
 template <typename T>
 bool grow(T **p, size_t *cap, size_t bytes) {
   return ensure_dev(reinterpret_cast<void **>(p), cap, bytes);
+}
+
+// the slot's scratch for `bytes` (nullptr and true when none is needed)
+bool slot_scratch(Slot &s, size_t bytes, void **out) {
+  *out = nullptr;
+  if (bytes == 0) return true;
+  if (!grow(&s.d_scr, &s.cap_scr, bytes)) return false;
+  *out = s.d_scr;
+  return true;
 }
 
 bool ok(hipError_t e, const char *what) {
@@ -189,9 +204,9 @@ NPRSResult ECCR_AMD_encode_host_batch(unsigned long nv, const uint8_t *h_payload
     const size_t cb = batch - c0 < chunk ? batch - c0 : chunk;
     if (!grow(&s.d_a, &s.cap_a, chunk * dps) || !grow(&s.d_b, &s.cap_b, chunk * nv * dss))
       return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
-    ScratchLease lease(d, encode_scratch_bytes(p, plen, cb), s.stream);  // slots never share it concurrently
-    if (!lease.ok()) return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
-    void *scratch = lease.ptr();
+    void *scratch = nullptr;
+    if (!slot_scratch(s, encode_scratch_bytes(p, plen, cb), &scratch))
+      return res(NPRS_RESULT_UNKNOWN_CODE_PARAM);
     const uint8_t *hp = h_payloads + c0 * pstride;
     uint8_t *hs = h_shards + c0 * nv * sstride;
     const hipError_t up =
@@ -233,6 +248,8 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
   std::vector<uint32_t> seen(nv, 0);
   std::vector<uint64_t> phash(batch);
   std::vector<uint32_t> pcount(batch);
+  std::vector<uint64_t> term(nv);  // mix64 of each index, once per call
+  for (unsigned long v = 0; v < nv; ++v) term[v] = mix64(v);
   for (unsigned long b = 0; b < batch; ++b) {
     unsigned long distinct = 0;
     uint64_t h = 0;
@@ -247,7 +264,7 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
       if (seen[v] != b + 1) {
         seen[v] = uint32_t(b + 1);
         ++distinct;
-        h += mix64(v);
+        h += term[v];
       }
     }
     if (distinct < p.k) return res(NPRS_RESULT_NOT_ENOUGH_CHUNKS);
@@ -275,7 +292,11 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
     if (!ok(hipEventSynchronize(s.staged), "staging reuse")) return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
     s.h_pat.resize(cb);
     s.h_rows.clear();
-    std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;
+    s.h_rows.reserve(cb * p.n);
+    // hash -> first pattern with it; further ones chained through next_pat
+    std::unordered_map<uint64_t, uint32_t> by_hash;
+    by_hash.reserve(cb);
+    std::vector<int32_t> next_pat;
     std::vector<uint32_t> pat_count;  // distinct indices per pattern
     uint32_t npat = 0;
     for (size_t j = 0; j < cb; ++j) {
@@ -286,19 +307,21 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
         continue;
       }
       int32_t found = -1;
-      auto &cands = by_hash[phash[b]];
-      for (uint32_t q : cands) {  // equal sets: same size and every index of b in q's row
+      const auto head = by_hash.find(phash[b]);
+      const int32_t first = head == by_hash.end() ? -1 : int32_t(head->second);
+      for (int32_t q = first; q >= 0; q = next_pat[q]) {  // equal sets: same size, every index of b in q's row
         const uint8_t *row = s.h_rows.data() + size_t(q) * p.n;
         bool same = pat_count[q] == pcount[b];
         for (unsigned long t = 0; t < cnt && same; ++t) same = row[ix[t]] != 0;
         if (same) {
-          found = int32_t(q);
+          found = q;
           break;
         }
       }
       if (found < 0) {
         found = int32_t(npat++);
-        cands.push_back(uint32_t(found));
+        next_pat.push_back(first);  // new head of the hash's chain
+        by_hash[phash[b]] = uint32_t(found);
         pat_count.push_back(pcount[b]);
         s.h_rows.resize(size_t(npat) * p.n, 0);
         uint8_t *row = s.h_rows.data() + size_t(found) * p.n;
@@ -306,9 +329,9 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
       }
       s.h_pat[j] = uint32_t(found);
     }
-    ScratchLease lease(d, reconstruct_scratch_bytes(p, slen, cb), s.stream);  // slots never share it concurrently
-    if (!lease.ok()) return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-    void *scratch = lease.ptr();
+    void *scratch = nullptr;
+    if (!slot_scratch(s, reconstruct_scratch_bytes(p, slen, cb), &scratch))
+      return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
     bool good =
         ok(hipMemcpyAsync(s.d_a, h_shards + c0 * cnt * sstride, cb * cnt * sstride,
                           hipMemcpyHostToDevice, s.stream),
