@@ -56,6 +56,14 @@ bool hip_check(hipError_t e, const char *what) {
 // copy is one linear transfer (a 2-D copy of narrow rows costs ~10 us per row)
 inline size_t dev_pitch(size_t sl) { return (sl + 15) / 16 * 16; }
 
+// Calls whose input and output together stay below this run the kernel on
+// the pinned staging buffers themselves (device-mapped host memory, read and
+// written over PCIe): no copy commands, so a small call costs one launch and
+// one synchronisation instead of three commands.  Kernel launches acquire
+// and release at system scope, so the host's staging writes are seen by the
+// kernel and its results by the host after the synchronisation.
+constexpr size_t kDirectBytes = size_t(64) << 10;
+
 // host -> device -> host encode of one payload into pinned h_out [nv][dev_pitch(sl)]
 bool encode_host(const CodeParams &p, const uint8_t *payload, size_t len, HostCtx *c,
                  size_t *sl_out) {
@@ -64,6 +72,20 @@ bool encode_host(const CodeParams &p, const uint8_t *payload, size_t len, HostCt
   const size_t sl = shard_len(p.k, len);
   const size_t dstride = dev_pitch(sl);
   const size_t out_bytes = size_t(p.nv) * dstride;
+  if (len + out_bytes <= kDirectBytes) {
+    if (!ensure_host(&c->h_in, &c->h_in_cap, len) || !ensure_host(&c->h_out, &c->h_out_cap, out_bytes))
+      return false;
+    ScratchLease lease(d, encode_scratch_bytes(p, len, 1), c->stream);
+    if (!lease.ok()) return false;
+    std::memcpy(c->h_in, payload, len);
+    if (!hip_check(launch_encode(p, device_tables(d), c->h_in, len, len, 1, c->h_out, dstride,
+                                 lease.ptr(), c->stream),
+                   "encode launch") ||
+        !hip_check(hipStreamSynchronize(c->stream), "encode"))
+      return false;
+    *sl_out = sl;
+    return true;
+  }
   if (!ensure_host(&c->h_in, &c->h_in_cap, len) ||
       !ensure_dev(reinterpret_cast<void **>(&c->d_in), &c->d_in_cap, len) ||
       !ensure_host(&c->h_out, &c->h_out_cap, out_bytes) ||
@@ -99,13 +121,18 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
   bool all_systematic = true;
   for (uint32_t y = 0; y < p.k; ++y) all_systematic &= present[y] != 0;
   (void)in_bytes;
-  if (!hip_check(hipMemcpyAsync(c->d_in, c->h_in, size_t(p.nv) * dstride, hipMemcpyHostToDevice,
-                                c->stream),
-                 "H2D"))
+  // small calls: the kernels read the staged shards and write the payload
+  // in pinned host memory (kDirectBytes)
+  const bool direct = size_t(p.nv) * dstride + out_bytes <= kDirectBytes;
+  const uint8_t *src = direct ? c->h_in : c->d_in;
+  uint8_t *dst = direct ? c->h_out : c->d_out;
+  if (!direct && !hip_check(hipMemcpyAsync(c->d_in, c->h_in, size_t(p.nv) * dstride,
+                                           hipMemcpyHostToDevice, c->stream),
+                            "H2D"))
     return false;
   if (all_systematic) {
     // every systematic shard is present: decode == interleave (exact)
-    if (!hip_check(launch_systematic(p, c->d_in, sl, dstride, 1, c->d_out, out_bytes, c->stream),
+    if (!hip_check(launch_systematic(p, src, sl, dstride, 1, dst, out_bytes, c->stream),
                    "systematic launch"))
       return false;
   } else {
@@ -115,20 +142,20 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
     ScratchLease lease(d, reconstruct_scratch_bytes(p, sl, 1), c->stream);
     if (!lease.ok()) return false;
     void *scratch = lease.ptr();
-    if (!hip_check(launch_reconstruct(p, device_tables(d), c->d_in, sl, dstride, loc->d_present,
-                                      loc->d_elog, nullptr, 1, c->d_out, out_bytes, scratch,
+    if (!hip_check(launch_reconstruct(p, device_tables(d), src, sl, dstride, loc->d_present,
+                                      loc->d_elog, nullptr, 1, dst, out_bytes, scratch,
                                       c->stream),
                    "reconstruct launch"))
       return false;
     // `loc` is released only after the stream has finished with it
-    return hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost,
-                                    c->stream),
-                     "D2H") &&
+    return (direct || hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes,
+                                               hipMemcpyDeviceToHost, c->stream),
+                                "D2H")) &&
            hip_check(hipStreamSynchronize(c->stream), "reconstruct");
   }
-  return hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost,
-                                  c->stream),
-                   "D2H") &&
+  return (direct || hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost,
+                                             c->stream),
+                              "D2H")) &&
          hip_check(hipStreamSynchronize(c->stream), "reconstruct");
 }
 

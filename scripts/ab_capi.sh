@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out/ab_capi
 for rep in 1 2; do
-  LD_LIBRARY_PATH=$PWD/scripts/micro/base_lib timeout -k 10 400 scripts/micro/capi_bench > gpurun_out/ab_capi/base_$rep.jsonl || exit 1
+  LD_LIBRARY_PATH=$PWD/scripts/micro/${BASE:-base_lib} timeout -k 10 400 scripts/micro/capi_bench > gpurun_out/ab_capi/base_$rep.jsonl || exit 1
   timeout -k 10 400 scripts/micro/capi_bench > gpurun_out/ab_capi/main_$rep.jsonl || exit 1
 done
 python3 - <<'PY'
