@@ -264,7 +264,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   // mul_index(E[row]), low half 0xFFFF = absent.  Loaded one tile ahead so the
   // gather's table loads wait on one global latency instead of two.
   // m[2], m[3]: the output rows y = 4 lane + q (q = 0..3) of phase 5, 16 bits
-  // each: 0xFFFF = present (copied from the shard), else mul_index(E[y]) (the
+  // each: 0xFFFF = present (copied from the staged row), else mul_index(E[y]) (the
   // erased value is scaled by E[y]; y < 256 < nv always holds for n = 1024).
   auto load_meta = [&](uint64_t tl, uint32_t tid, uint32_t (&m)[4]) {
     const uint64_t bb = tl / tiles_pp, pt = pattern ? pattern[bb] : bb;
@@ -305,26 +305,24 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     Tab RT[2];
     const uint64_t avail = slen - 2 * col0;  // bytes of a row inside the tile
     const auto load_row = [&](int half) __attribute__((always_inline)) {
-      {
-        const uint8_t *row = SH + uint64_t(meta[half] >> 16) * sstride + 2 * col0;
-        if (avail >= 64) {
+      const uint8_t *row = SH + uint64_t(meta[half] >> 16) * sstride + 2 * col0;
+      if (avail >= 64) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint4 d = reinterpret_cast<const uint4 *>(row)[q];
-            w[half][4 * q] = d.x;
-            w[half][4 * q + 1] = d.y;
-            w[half][4 * q + 2] = d.z;
-            w[half][4 * q + 3] = d.w;
-          }
-        } else {
-#pragma unroll
-          for (int q = 0; q < 16; ++q) w[half][q] = 0;
-#pragma unroll
-          for (int e = 0; e < 64; ++e)  // constant trip count: w stays in registers
-            if (uint64_t(e) < avail) w[half][e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
+        for (int q = 0; q < 4; ++q) {
+          const uint4 d = reinterpret_cast<const uint4 *>(row)[q];
+          w[half][4 * q] = d.x;
+          w[half][4 * q + 1] = d.y;
+          w[half][4 * q + 2] = d.z;
+          w[half][4 * q + 3] = d.w;
         }
-        load_tab(t.mtab, meta[half] & 0xffffu, RT[half]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) w[half][q] = 0;
+#pragma unroll
+        for (int e = 0; e < 64; ++e)  // constant trip count: w stays in registers
+          if (uint64_t(e) < avail) w[half][e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
       }
+      load_tab(t.mtab, meta[half] & 0xffffu, RT[half]);
     };
     if ((meta[0] & 0xffffu) != 0xffffu) load_row(0);
     STAMP(0);
