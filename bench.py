@@ -57,6 +57,34 @@ def pmc_traffic(kernel, nv, plen, cnt, batch):
     return None, None
 
 
+# waves per SIMD of the dominant kernels (launch shapes in csrc/): the SQ
+# counters' per-wave ACTIVE_INST_ANY fraction times this is the share of SIMD
+# cycles that issued an instruction
+_WAVES_PER_SIMD = {"reconstruct": ("reconstruct_n1024", 2), "encode": ("encode_k256<1024>", 4)}
+
+
+def sq_issue(kernel, nv):
+    """SIMD issue fraction of `kernel` from the committed SQ counter summary
+    (scripts/pmc_sq.sh + scripts/sq_summary.py, newest profiles/rNN), measured
+    on the default workload shape (nv = 1024): the kernels are bounded by
+    instruction issue, not HBM."""
+    import glob
+    name, waves = _WAVES_PER_SIMD.get(kernel, (None, 0))
+    if name is None or nv != 1024:
+        return None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "sq_counters.json")),
+                       reverse=True):
+        try:
+            with open(path) as f:
+                k = json.load(f)["kernels"][name]
+            return {"simd_issue_frac": round(k["frac_active_inst_any"] * waves, 3),
+                    "valu_frac": round(k["frac_active_valu"] * waves, 3),
+                    "source": os.path.relpath(path, ROOT)}
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -299,7 +327,8 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved / 1e9, 2),
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
-                     "bytes_per_launch": b_dom, "avg_launch_ms": round(t_dom, 4)},
+                     "bytes_per_launch": b_dom, "avg_launch_ms": round(t_dom, 4),
+                     "issue": sq_issue(dom, nv)},
         "kernels_ms": {"encode": round(t_enc, 4), "error_locator": round(t_loc, 4),
                        "reconstruct": round(t_rec, 4)},
         "encode_GiBps": round(world * B * plen / (t_enc * 1e-3) / 2**30, 3),
