@@ -99,15 +99,9 @@ __host__ __device__ constexpr uint32_t tlin(uint32_t idx) {
   return ((idx >> 4) << 8) | (((idx ^ (idx >> 4) ^ (idx >> 8)) & 15) << 4);
 }
 
-__device__ __forceinline__ void tab_at(const uint8_t *lds, uint32_t lin, Tab &T) {
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(lds + q * Tabs::kPlane + lin);
-    T.t[4 * q] = v.x;
-    T.t[4 * q + 1] = v.y;
-    T.t[4 * q + 2] = v.z;
-    T.t[4 * q + 3] = v.w;
-  }
+// the tables are the first thing in the kernel's LDS (address 0: lds_tab_abs)
+__device__ __forceinline__ void tab_at(const uint8_t *, uint32_t lin, Tab &T) {
+  lds_tab_abs<Tabs::kPlane>(lin, T);
 }
 
 // inverse radix-16 pass over position bits b0..b0+3: pos(r) = lane part | (r << b0),

@@ -75,6 +75,25 @@ struct Tab {
   uint32_t t[20];
 };
 
+// One 80-byte multiply table from LDS at absolute LDS address `a` (plane 0;
+// planes `plane` bytes apart), planes loaded last-used first so the first
+// multiply waits once.  The big-LDS kernels have no static LDS (checked by
+// prepare_kernel), so their dynamic LDS starts at address 0 and a table
+// address is a per-lane base XOR a compile-time value: no add of the LDS base
+// per table (the base is a link-time symbol the compiler cannot fold).
+template <int PLANE>
+__device__ __forceinline__ void lds_tab_abs(uint32_t a, Tab &T) {
+#pragma unroll
+  for (int q = 4; q >= 0; --q) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u v = *(const __attribute__((address_space(3))) v4u *)(uintptr_t(a + q * PLANE));
+    T.t[4 * q] = v.x;
+    T.t[4 * q + 1] = v.y;
+    T.t[4 * q + 2] = v.z;
+    T.t[4 * q + 3] = v.w;
+  }
+}
+
 __device__ __forceinline__ void load_tab(const MulTab *__restrict__ mt, uint32_t c, Tab &T) {
   const uint4 *p = reinterpret_cast<const uint4 *>(mt + c);
 #pragma unroll

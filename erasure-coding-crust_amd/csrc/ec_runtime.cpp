@@ -126,6 +126,11 @@ hipError_t prepare_kernel(const void *fn, int lds_bytes, int *cus) {
   }
   bool &done = prepared[{dev, fn}];
   if (!done && lds_bytes > 65536) {
+    // these kernels address their multiply tables by absolute LDS address,
+    // assuming their dynamic LDS starts at 0, i.e. no static LDS (lds_tab_at)
+    hipFuncAttributes attr{};
+    if (const hipError_t e = hipFuncGetAttributes(&attr, fn); e != hipSuccess) return e;
+    if (attr.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
     const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
     if (e != hipSuccess) return e;
   }
