@@ -144,7 +144,9 @@ struct NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long n_validators,
 /* Cap on one per-device scratch allocation in bytes (0 = no cap, the
  * default).  A call whose shape needs more fails with UNKNOWN_CODE_PARAM
  * (encode) / UNKNOWN_RECONSTRUCTION (reconstruct) exactly as when hipMalloc
- * runs out of memory; nothing is launched.  For memory-constrained
+ * runs out of memory; nothing is launched.  Applies to the per-call C ABI
+ * and the device-batch calls; the host-batch pipeline's slots own their
+ * (chunk-sized) scratch and are not capped.  For memory-constrained
  * deployments and the failure-path tests. */
 void ECCR_AMD_set_scratch_limit(unsigned long bytes);
 
