@@ -178,6 +178,17 @@ __device__ __forceinline__ void swap_bit(uint32_t &x, uint32_t &y, int b, bool h
 
 __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ? 0u : c; }
 
+// The two waves of a SIMD (w, w + 4) take turns at the higher issue priority
+// (pass A: w + 4, pass B: w, pass C to the FFT: w + 4, output: equal), so
+// neither runs far ahead and then idles at the tile barrier while the other
+// finishes alone (the arbiter otherwise favours the older wave throughout).
+// A/B at B = 2048: 7.06 -> 7.01 ms; one fixed priority for the whole
+// transform 7.08, four turns 7.09.
+__device__ __forceinline__ void prio_lead(bool lead) {
+  if (lead) __builtin_amdgcn_s_setprio(2);
+  else __builtin_amdgcn_s_setprio(0);
+}
+
 }  // namespace
 
 // Gather order of a payload's received rows (its erasure pattern), per
@@ -371,6 +382,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         s.l[r] = x.x;
         s.h[r] = x.y;
       }
+      prio_lead(wave & 4);
       ipass4<0>(s, tabs, tlin(16 * lane));
 #pragma unroll
       for (int r = 0; r < 16; ++r) lds_st2(la ^ raddr(r), make_uint2(s.l[r], s.h[r]));
@@ -386,6 +398,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         s.l[r] = x.x;
         s.h[r] = x.y;
       }
+      prio_lead(!(wave & 4));
       ipass4<4>(s, tabs, tlin((lane >> 4) << 8));
 #pragma unroll
       for (int r = 0; r < 16; ++r) lds_st2(lb ^ raddr(uint32_t(r) << 4), make_uint2(s.l[r], s.h[r]));
@@ -421,6 +434,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       }
     }
 
+    prio_lead(wave & 4);
     STAMP(4);
     // ---- phases 3 + 4a: formal derivative (poly_encoder.hpp:195-215) and FFT
     // stages 9, 8 (afft, additive_fft.hpp:121-141) for the outputs y < 256 only.
@@ -557,6 +571,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       fb(0, 1, T[0]);  // stage 0
       fb(2, 3, T[1]);
     }
+    __builtin_amdgcn_s_setprio(0);
     STAMP(8);
     STAMP(9);
 
