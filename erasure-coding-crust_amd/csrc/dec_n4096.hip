@@ -189,6 +189,10 @@ reconstruct_n4096(
         Qq.l[r] = x.x;
         Qq.h[r] = x.y;
       }
+      // the two waves of a SIMD (w, w + 4) alternate the higher issue
+      // priority from quarter to quarter (as reconstruct_n1024's passes)
+      if (((wave >> 2) ^ uint32_t(q)) & 1) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(0);
       if (q == 0) ifft1024<true>(Qq, tabs, my, lq);  // -> layout C; quarter 0 is at index 0
       else ifft1024<false>(Qq, tabs, my, lq);
       __builtin_amdgcn_sched_barrier(0);
@@ -253,6 +257,7 @@ reconstruct_n4096(
     // k_q folded on the host from skews 1023 / 2047 / 3071: n4096_lin()).
     // D in closed form (poly_encoder.hpp:195-215) over bits 0..9, in place:
     // lane = p0..p5, r = (p8, p9, p6, p7).
+    __builtin_amdgcn_s_setprio(0);
     derivative<LC, 10, KB>(P, lane);  // at the registers reaching y < k only
     S16 Y;
 #pragma unroll
