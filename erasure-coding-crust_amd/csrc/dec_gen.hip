@@ -244,8 +244,14 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
       asm volatile("" : "+v"(l));
       return tlin(((l >> 4) << 8) & NM);
     };
+    // the two waves of a SIMD (w, w + 4) take turns at the higher issue
+    // priority (pass A: w + 4, then w), as in reconstruct_n1024
+    if (wave & 4) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(0);
     ipassg<0, 4, L>(s, tabs, lbA());
     __builtin_amdgcn_sched_barrier(0);
+    if (wave & 4) __builtin_amdgcn_s_setprio(0);
+    else __builtin_amdgcn_s_setprio(2);
     exchange<LA, LB>(s, my, lane);
     if constexpr (L <= 8) {
       ipassg<4, L - 4, L>(s, tabs, lbB());
@@ -263,6 +269,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
       __builtin_amdgcn_sched_barrier(0);
       fft_restricted<LC, L, KB>(s, tabs, lane);
     }
+    __builtin_amdgcn_s_setprio(0);
 #pragma unroll
     for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(s.l[r]), "+v"(s.h[r]));  // finished here, not sunk into the output
 
