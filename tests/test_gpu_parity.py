@@ -323,6 +323,62 @@ def _prefilled(shape, fill=0xAA):
     return torch.full(shape, fill, dtype=torch.uint8, device="cuda")
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_batch_random_shapes_and_runs(oracle, seed):
+    """Random n_validators (every fast reconstruct and the generic kernel) with
+    present sets shaped against the gather order (gather_order: present rows
+    first, wave-major): a random subset of random size in [k, nv], one
+    contiguous run, a strided set and the last rows only -- so whole waves
+    of slots are full, empty or partly present -- on the device batch path,
+    compared with the oracle; outputs prefilled with 0xAA."""
+    import torch
+    rng = np.random.default_rng(1234 + seed)
+    for nv in [int(x) for x in rng.choice(
+            [46, 70, 129, 200, 257, 383, 513, 700, 800, 1000, 1024, 1100, 1700, 2049, 2700, 3071, 4000],
+            3, replace=False)]:
+        n, k, thr = E.code_params(nv)
+        plen = int(rng.integers(1, 3 * 2 * k))
+        sl = E.shard_len(nv, plen)
+        ss = (sl + 15) // 16 * 16
+
+        def mask(idx):
+            m = np.zeros(n, dtype=np.uint8)
+            m[np.asarray(sorted(set(int(x) for x in idx)), dtype=np.int64)] = 1
+            return m
+
+        cnt = int(rng.integers(k, nv + 1))
+        start = int(rng.integers(0, nv - k + 1))
+        step = int(rng.integers(2, 4))
+        strided = list(range(0, nv, step))[:max(k, 1)]
+        strided += [i for i in range(nv) if i % step][: max(0, k - len(strided))]
+        rows = [mask(rng.permutation(nv)[:cnt]), mask(range(start, start + k)), mask(strided),
+                mask(range(nv - k, nv))]
+        batch = len(rows)
+        pay = np.stack([synth.payload(777 + 31 * seed + b + nv, plen) for b in range(batch)])
+        pres = np.stack(rows)
+        d_pay = torch.from_numpy(pay).cuda()
+        d_sh = _prefilled((batch, nv, ss))
+        d_pr = torch.from_numpy(pres).cuda()
+        d_el = torch.zeros((batch, n), dtype=torch.int16, device="cuda")
+        d_out = _prefilled((batch, sl * k))
+        E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+        torch.cuda.synchronize()
+        sh_np = d_sh.cpu().numpy()
+        for b in range(batch):
+            gone = np.where(pres[b][:nv] == 0)[0]
+            if len(gone):
+                d_sh[b, torch.from_numpy(gone).cuda()] = 0x5C
+        E.error_locator(nv, d_pr, batch, d_el)
+        E.reconstruct_batch(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k)
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy()
+        for b in range(batch):
+            shards = [sh_np[b, i, :sl].tobytes() if pres[b][i] else None for i in range(nv)]
+            want = oracle.reconstruct(nv, shards)
+            assert out[b].tobytes() == want, (nv, plen, b)
+            assert out[b, :plen].tobytes() == pay[b].tobytes()
+
+
 @pytest.mark.parametrize("nv,plen,pad", [
     (1024, 70001, 64), (800, 33333, 16),                # reconstruct_n1024 (nv = n and nv < n)
     (1500, 70001, 64), (2048, 40001, 16),               # reconstruct_n4096, 2 halves, k = 256 / 512
