@@ -499,11 +499,26 @@ def test_locator_cache_per_call(oracle):
 README_SIZES = [15, 300, 5000, 100_000, 1_000_000, 10_000_000]  # README.md:50-84
 
 
-def _host_roundtrip(oracle, nv, plen, batch, chunk, seed, shared=False, check_all=True):
+def _pinned_like(a):
+    """a copy of numpy array `a` in pinned host memory (ECCR_AMD_host_alloc),
+    viewed as numpy; freed with the returned handle"""
+    import ctypes
+    ptr = E.lib().ECCR_AMD_host_alloc(a.nbytes)
+    assert ptr
+    buf = (ctypes.c_uint8 * a.nbytes).from_address(ptr)
+    v = np.frombuffer(buf, dtype=a.dtype).reshape(a.shape)
+    v[...] = a
+    return v, ptr
+
+
+def _host_roundtrip(oracle, nv, plen, batch, chunk, seed, shared=False, check_all=True,
+                    pinned=False):
     n, k, thr = E.code_params(nv)
     sl = E.shard_len(nv, plen)
     pay = np.stack([synth.payload(seed + b, plen) for b in range(batch)])
     sh = np.full((batch, nv, sl), 0xAA, dtype=np.uint8)
+    if pinned:  # pinned host buffers (device-mapped): the pipeline's fast paths
+        return _host_roundtrip_pinned(oracle, nv, plen, batch, chunk, seed, pay, sh)
     E.encode_host_batch(nv, pay, plen, plen, batch, sh, sl, chunk)
     for b in (range(batch) if check_all else [0, batch - 1]):
         assert b"".join(oracle.encode(nv, pay[b].tobytes())) == sh[b].tobytes(), (plen, b)
@@ -522,6 +537,44 @@ def _host_roundtrip(oracle, nv, plen, batch, chunk, seed, shared=False, check_al
         kk = set(int(x) for x in idx[b])
         keep = [sh[b][i].tobytes() if i in kk else None for i in range(nv)]
         assert out[b].tobytes() == oracle.reconstruct(nv, keep), (plen, b)
+
+
+def _host_roundtrip_pinned(oracle, nv, plen, batch, chunk, seed, pay, sh):
+    n, k, thr = E.code_params(nv)
+    sl = E.shard_len(nv, plen)
+    held = []
+    try:
+        pay_p, q = _pinned_like(pay)
+        held.append(q)
+        sh_p, q = _pinned_like(sh)
+        held.append(q)
+        E.encode_host_batch(nv, pay_p, plen, plen, batch, sh_p, sl, chunk)
+        for b in range(batch):
+            assert b"".join(oracle.encode(nv, pay[b].tobytes())) == sh_p[b].tobytes(), (plen, b)
+        idx = np.stack([synth.present_set(seed + 7 * b, nv, thr) for b in range(batch)]).astype(np.uint16)
+        comp_p, q = _pinned_like(np.stack([sh_p[b][idx[b]] for b in range(batch)]))
+        held.append(q)
+        idx_p, q = _pinned_like(idx)
+        held.append(q)
+        out_p, q = _pinned_like(np.full((batch, sl * k), 0xAA, dtype=np.uint8))
+        held.append(q)
+        E.reconstruct_host_batch(nv, comp_p, sl, sl, idx_p, thr, batch, out_p, sl * k, chunk)
+        for b in range(batch):
+            kk = set(int(x) for x in idx[b])
+            keep = [sh_p[b][i].tobytes() if i in kk else None for i in range(nv)]
+            assert out_p[b].tobytes() == oracle.reconstruct(nv, keep), (plen, b)
+            assert out_p[b][:plen].tobytes() == pay[b].tobytes(), (plen, b)
+    finally:
+        for q in held:
+            E.lib().ECCR_AMD_host_free(q)
+
+
+@pytest.mark.parametrize("nv,plen,batch,chunk", [(1024, 1_000_000, 7, 2), (1024, 300, 50, 0),
+                                                  (600, 100_001, 9, 4), (4096, 65_537, 5, 0)])
+def test_host_batch_pinned(oracle, nv, plen, batch, chunk):
+    """Host batches in pinned memory (ECCR_AMD_host_alloc, as a real caller
+    allocates them for full PCIe rate), odd sizes included, vs the oracle."""
+    _host_roundtrip(oracle, nv, plen, batch, chunk, seed=plen + nv, pinned=True)
 
 
 @pytest.mark.parametrize("plen,batch", [(15, 300), (300, 100), (10_000_000, 2)])
