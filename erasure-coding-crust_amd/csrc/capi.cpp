@@ -24,6 +24,11 @@ using namespace ecamd;
 
 namespace {
 
+struct Workspace {  // caller-owned device scratch (the *_ws batch entry points)
+  void *ptr;
+  size_t bytes;
+};
+
 NPRSResult result(NPRSResult_Tag tag) {
   NPRSResult r;
   std::memset(&r, 0, sizeof r);
@@ -380,9 +385,43 @@ NPRSResult ECCR_AMD_init_device(void) {
   return device_state() ? result(NPRS_RESULT_OK) : result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
 }
 
-NPRSResult ECCR_AMD_encode_batch(unsigned long nv, const uint8_t *d_payloads, unsigned long plen,
-                                 unsigned long pstride, unsigned long batch, uint8_t *d_shards,
-                                 unsigned long sstride, void *stream) {
+}  // extern "C"
+
+namespace {
+// Device scratch of one batch call: the caller's workspace (the *_ws entry
+// points: no allocation, no event, no host synchronisation, so the call can be
+// captured into a hipGraph once the shape has run once) or else the
+// per-device lease.  `ok` false = too small / misaligned workspace or a failed
+// allocation: nothing may be launched.
+struct BatchScratch {
+  ScratchLease lease;
+  void *p = nullptr;
+  bool ok = false;
+  BatchScratch(DeviceState *d, size_t need, hipStream_t s, const Workspace *ws)
+      : lease(d, ws ? 0 : need, s) {
+    if (!ws) {
+      ok = lease.ok();
+      p = lease.ptr();
+    } else if (need == 0) {
+      ok = true;
+    } else if (!ws->ptr || ws->bytes < need || reinterpret_cast<uintptr_t>(ws->ptr) % 256 != 0) {
+      set_error("erasure_coding_crust(amd): workspace of " + std::to_string(ws->bytes) +
+                " bytes (256-B aligned required) is below the " + std::to_string(need) +
+                " bytes this shape needs (ECCR_AMD_*_workspace_bytes)");
+    } else {
+      ok = true;
+      p = ws->ptr;
+    }
+  }
+};
+
+size_t locator_scratch_bytes(size_t batch) {
+  return batch <= 1 ? 0 : (batch * 4 + 255) / 256 * 256 + dedup_scratch_bytes(batch);
+}
+
+NPRSResult encode_batch(unsigned long nv, const uint8_t *d_payloads, unsigned long plen,
+                        unsigned long pstride, unsigned long batch, uint8_t *d_shards,
+                        unsigned long sstride, hipStream_t s, const Workspace *ws) {
   CodeParams p;
   NPRSResult r = params_or_error(nv, &p);
   if (r.tag != NPRS_RESULT_OK) return r;
@@ -390,25 +429,23 @@ NPRSResult ECCR_AMD_encode_batch(unsigned long nv, const uint8_t *d_payloads, un
   if (sstride < shard_len(p.k, plen) || pstride < plen) return result(NPRS_RESULT_BAD_PAYLOAD);
   DeviceState *d = device_state();
   if (!d) return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
-  ScratchLease lease(d, encode_scratch_bytes(p, plen, batch), static_cast<hipStream_t>(stream));
-  if (!lease.ok()) return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
-  void *scratch = lease.ptr();
+  BatchScratch sc(d, encode_scratch_bytes(p, plen, batch), s, ws);
+  if (!sc.ok) return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
   if (!hip_check(launch_encode(p, device_tables(d), d_payloads, plen, pstride, batch, d_shards,
-                               sstride, scratch, static_cast<hipStream_t>(stream)),
+                               sstride, sc.p, s),
                  "encode launch"))
     return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
   return result(NPRS_RESULT_OK);
 }
 
-NPRSResult ECCR_AMD_error_locator(unsigned long nv, const uint8_t *d_present, unsigned long batch,
-                                  uint16_t *d_err_log, void *stream) {
+NPRSResult error_locator(unsigned long nv, const uint8_t *d_present, unsigned long batch,
+                         uint16_t *d_err_log, hipStream_t s, const Workspace *ws) {
   CodeParams p;
   NPRSResult r = params_or_error(nv, &p);
   if (r.tag != NPRS_RESULT_OK) return r;
   DeviceState *d = device_state();
   const uint16_t *fold = d ? device_fold(d, p.n) : nullptr;
   if (!fold) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-  const hipStream_t s = static_cast<hipStream_t>(stream);
   if (batch <= 1) {
     if (!hip_check(launch_error_locator(p, d_present, batch, fold, nullptr, d_err_log, s),
                    "error locator launch"))
@@ -417,16 +454,81 @@ NPRSResult ECCR_AMD_error_locator(unsigned long nv, const uint8_t *d_present, un
   }
   // one locator per distinct pattern (§8f row 3), then copied to its followers
   const size_t pat_bytes = (batch * 4 + 255) / 256 * 256;
-  ScratchLease lease(d, pat_bytes + dedup_scratch_bytes(batch), s);
-  if (!lease.ok()) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-  uint32_t *pat = static_cast<uint32_t *>(lease.ptr());
-  void *work = static_cast<uint8_t *>(lease.ptr()) + pat_bytes;
+  BatchScratch sc(d, locator_scratch_bytes(batch), s, ws);
+  if (!sc.ok) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  uint32_t *pat = static_cast<uint32_t *>(sc.p);
+  void *work = static_cast<uint8_t *>(sc.p) + pat_bytes;
   if (!hip_check(launch_dedup_patterns(p, d_present, batch, pat, work, s), "pattern dedup") ||
       !hip_check(launch_error_locator(p, d_present, batch, fold, pat, d_err_log, s),
                  "error locator launch") ||
       !hip_check(launch_broadcast_locators(p, pat, batch, d_err_log, s), "locator broadcast"))
     return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
   return result(NPRS_RESULT_OK);
+}
+
+NPRSResult reconstruct_batch(unsigned long nv, const uint8_t *d_shards, unsigned long slen,
+                             unsigned long sstride, const uint8_t *d_present,
+                             const uint16_t *d_err_log, const uint32_t *d_pattern,
+                             unsigned long batch, uint8_t *d_out, unsigned long ostride,
+                             hipStream_t s, const Workspace *ws) {
+  CodeParams p;
+  NPRSResult r = params_or_error(nv, &p);
+  if (r.tag != NPRS_RESULT_OK) return r;
+  if (slen % 2 != 0) return result(NPRS_RESULT_UNEVEN_LENGTH);
+  if (sstride < slen || ostride < slen * p.k) return result(NPRS_RESULT_NON_UNIFORM_CHUNKS);
+  DeviceState *d = device_state();
+  if (!d) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  BatchScratch sc(d, reconstruct_scratch_bytes(p, slen, batch), s, ws);
+  if (!sc.ok) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  if (!hip_check(launch_reconstruct(p, device_tables(d), d_shards, slen, sstride, d_present,
+                                    d_err_log, d_pattern, batch, d_out, ostride, sc.p, s),
+                 "reconstruct launch"))
+    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+  return result(NPRS_RESULT_OK);
+}
+}  // namespace
+
+extern "C" {
+
+NPRSResult ECCR_AMD_encode_batch(unsigned long nv, const uint8_t *d_payloads, unsigned long plen,
+                                 unsigned long pstride, unsigned long batch, uint8_t *d_shards,
+                                 unsigned long sstride, void *stream) {
+  return encode_batch(nv, d_payloads, plen, pstride, batch, d_shards, sstride,
+                      static_cast<hipStream_t>(stream), nullptr);
+}
+
+unsigned long ECCR_AMD_encode_workspace_bytes(unsigned long nv, unsigned long plen,
+                                              unsigned long batch) {
+  CodeParams p;
+  if (code_params(nv, &p) != ParamError::kOk || plen == 0) return 0;
+  return encode_scratch_bytes(p, plen, batch);
+}
+
+NPRSResult ECCR_AMD_encode_batch_ws(unsigned long nv, const uint8_t *d_payloads,
+                                    unsigned long plen, unsigned long pstride, unsigned long batch,
+                                    uint8_t *d_shards, unsigned long sstride, void *d_workspace,
+                                    unsigned long workspace_bytes, void *stream) {
+  const Workspace ws{d_workspace, workspace_bytes};
+  return encode_batch(nv, d_payloads, plen, pstride, batch, d_shards, sstride,
+                      static_cast<hipStream_t>(stream), &ws);
+}
+
+NPRSResult ECCR_AMD_error_locator(unsigned long nv, const uint8_t *d_present, unsigned long batch,
+                                  uint16_t *d_err_log, void *stream) {
+  return error_locator(nv, d_present, batch, d_err_log, static_cast<hipStream_t>(stream), nullptr);
+}
+
+unsigned long ECCR_AMD_error_locator_workspace_bytes(unsigned long nv, unsigned long batch) {
+  CodeParams p;
+  if (code_params(nv, &p) != ParamError::kOk) return 0;
+  return locator_scratch_bytes(batch);
+}
+
+NPRSResult ECCR_AMD_error_locator_ws(unsigned long nv, const uint8_t *d_present,
+                                     unsigned long batch, uint16_t *d_err_log, void *d_workspace,
+                                     unsigned long workspace_bytes, void *stream) {
+  const Workspace ws{d_workspace, workspace_bytes};
+  return error_locator(nv, d_present, batch, d_err_log, static_cast<hipStream_t>(stream), &ws);
 }
 
 NPRSResult ECCR_AMD_dedup_patterns(unsigned long nv, const uint8_t *d_present, unsigned long batch,
@@ -465,22 +567,26 @@ NPRSResult ECCR_AMD_reconstruct_batch_patterns(unsigned long nv, const uint8_t *
                                                const uint8_t *d_present, const uint16_t *d_err_log,
                                                const uint32_t *d_pattern, unsigned long batch,
                                                uint8_t *d_out, unsigned long ostride, void *stream) {
+  return reconstruct_batch(nv, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch,
+                           d_out, ostride, static_cast<hipStream_t>(stream), nullptr);
+}
+
+unsigned long ECCR_AMD_reconstruct_workspace_bytes(unsigned long nv, unsigned long slen,
+                                                   unsigned long batch) {
   CodeParams p;
-  NPRSResult r = params_or_error(nv, &p);
-  if (r.tag != NPRS_RESULT_OK) return r;
-  if (slen % 2 != 0) return result(NPRS_RESULT_UNEVEN_LENGTH);
-  if (sstride < slen || ostride < slen * p.k) return result(NPRS_RESULT_NON_UNIFORM_CHUNKS);
-  DeviceState *d = device_state();
-  if (!d) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-  ScratchLease lease(d, reconstruct_scratch_bytes(p, slen, batch), static_cast<hipStream_t>(stream));
-  if (!lease.ok()) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-  void *scratch = lease.ptr();
-  if (!hip_check(launch_reconstruct(p, device_tables(d), d_shards, slen, sstride, d_present,
-                                    d_err_log, d_pattern, batch, d_out, ostride, scratch,
-                                    static_cast<hipStream_t>(stream)),
-                 "reconstruct launch"))
-    return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-  return result(NPRS_RESULT_OK);
+  if (code_params(nv, &p) != ParamError::kOk) return 0;
+  return reconstruct_scratch_bytes(p, slen, batch);
+}
+
+NPRSResult ECCR_AMD_reconstruct_batch_ws(unsigned long nv, const uint8_t *d_shards,
+                                         unsigned long slen, unsigned long sstride,
+                                         const uint8_t *d_present, const uint16_t *d_err_log,
+                                         const uint32_t *d_pattern, unsigned long batch,
+                                         uint8_t *d_out, unsigned long ostride, void *d_workspace,
+                                         unsigned long workspace_bytes, void *stream) {
+  const Workspace ws{d_workspace, workspace_bytes};
+  return reconstruct_batch(nv, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch,
+                           d_out, ostride, static_cast<hipStream_t>(stream), &ws);
 }
 
 NPRSResult ECCR_AMD_reconstruct_batch(unsigned long nv, const uint8_t *d_shards,

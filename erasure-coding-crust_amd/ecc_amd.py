@@ -122,6 +122,13 @@ def lib():
             "ECCR_AMD_reconstruct_batch_patterns": (NPRSResult, [ul, vp, ul, ul, vp, vp, vp, ul, vp,
                                                                  ul, vp]),
             "ECCR_AMD_locator_cache_stats": (NPRSResult, [up, up]),
+            "ECCR_AMD_encode_workspace_bytes": (ul, [ul, ul, ul]),
+            "ECCR_AMD_error_locator_workspace_bytes": (ul, [ul, ul]),
+            "ECCR_AMD_reconstruct_workspace_bytes": (ul, [ul, ul, ul]),
+            "ECCR_AMD_encode_batch_ws": (NPRSResult, [ul, vp, ul, ul, ul, vp, ul, vp, ul, vp]),
+            "ECCR_AMD_error_locator_ws": (NPRSResult, [ul, vp, ul, vp, vp, ul, vp]),
+            "ECCR_AMD_reconstruct_batch_ws": (NPRSResult, [ul, vp, ul, ul, vp, vp, vp, ul, vp, ul,
+                                                           vp, ul, vp]),
             "ECCR_AMD_host_alloc": (vp, [ul]),
             "ECCR_AMD_host_free": (None, [vp]),
             "ECCR_AMD_encode_host_batch": (NPRSResult, [ul, vp, ul, ul, ul, vp, ul, ul]),
@@ -307,6 +314,43 @@ def reconstruct_batch_patterns(nv, d_shards, shard_len_, shard_stride, d_present
         nv, _p(d_shards), shard_len_, shard_stride, _p(d_present), _p(d_err_log),
         None if d_pattern is None else _p(d_pattern), batch, _p(d_out), out_stride,
         _stream(stream)), "reconstruct_batch_patterns")
+
+
+def workspace_bytes(nv, payload_len, batch):
+    """(encode, error_locator, reconstruct) device scratch bytes of a batch shape."""
+    sl = shard_len(nv, payload_len)
+    L = lib()
+    return (int(L.ECCR_AMD_encode_workspace_bytes(nv, payload_len, batch)),
+            int(L.ECCR_AMD_error_locator_workspace_bytes(nv, batch)),
+            int(L.ECCR_AMD_reconstruct_workspace_bytes(nv, sl, batch)))
+
+
+def _ws(ws):
+    return (None, 0) if ws is None else (_p(ws), ws.numel() if hasattr(ws, "numel") else ws.nbytes)
+
+
+def encode_batch_ws(nv, d_payloads, payload_len, payload_stride, batch, d_shards, shard_stride,
+                    ws, stream=None):
+    """encode_batch on caller-owned scratch `ws` (graph-capture-safe after one warm call)."""
+    wp, wb = _ws(ws)
+    _check(lib().ECCR_AMD_encode_batch_ws(nv, _p(d_payloads), payload_len, payload_stride, batch,
+                                          _p(d_shards), shard_stride, wp, wb, _stream(stream)),
+           "encode_batch_ws")
+
+
+def error_locator_ws(nv, d_present, batch, d_err_log, ws, stream=None):
+    wp, wb = _ws(ws)
+    _check(lib().ECCR_AMD_error_locator_ws(nv, _p(d_present), batch, _p(d_err_log), wp, wb,
+                                           _stream(stream)), "error_locator_ws")
+
+
+def reconstruct_batch_ws(nv, d_shards, shard_len_, shard_stride, d_present, d_err_log, batch,
+                         d_out, out_stride, ws, d_pattern=None, stream=None):
+    wp, wb = _ws(ws)
+    _check(lib().ECCR_AMD_reconstruct_batch_ws(
+        nv, _p(d_shards), shard_len_, shard_stride, _p(d_present), _p(d_err_log),
+        None if d_pattern is None else _p(d_pattern), batch, _p(d_out), out_stride, wp, wb,
+        _stream(stream)), "reconstruct_batch_ws")
 
 
 def locator_cache_stats():

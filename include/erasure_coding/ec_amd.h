@@ -4,15 +4,18 @@
  *
  * All pointers named d_* are device pointers on the codec's device; `stream`
  * is a hipStream_t (NULL = the legacy default stream).  Calls are asynchronous
- * on `stream` and the caller owns every buffer it passes.  They are NOT
- * graph-capture-safe in general: the first call per (device, kernel) sets a
- * kernel attribute; shapes that need device scratch (k = 1024 encodes, the
- * fast reconstructs' per-payload gather order (4 n bytes per payload), n > 4096
- * generic kernels, ECCR_AMD_error_locator / ECCR_AMD_dedup_patterns with
- * batch > 1) take a per-device scratch buffer that may be (re)allocated with
- * hipMalloc / hipFree and is ordered across streams with an event
- * (hipStreamWaitEvent, and hipEventSynchronize when it grows).  Warm a shape
- * up once outside capture.  Results are bit-exact with ec-cpp:
+ * on `stream` and the caller owns every buffer it passes.  The plain calls
+ * are NOT graph-capture-safe in general: shapes that need device scratch
+ * (k = 1024 encodes, the fast reconstructs' per-payload gather order (4 n
+ * bytes per payload), n > 4096 generic kernels, ECCR_AMD_error_locator /
+ * ECCR_AMD_dedup_patterns with batch > 1) take a per-device scratch buffer
+ * that may be (re)allocated with hipMalloc / hipFree and is ordered across
+ * streams with an event (hipStreamWaitEvent, and hipEventSynchronize when it
+ * grows).  The *_ws variants take caller-owned scratch instead (size from the
+ * matching *_workspace_bytes query) and then allocate, record and wait on
+ * nothing: after one call of a shape outside capture (the first call per
+ * (device, kernel) sets a kernel attribute and uploads the tables) they can be
+ * captured into a hipGraph and replayed.  Results are bit-exact with ec-cpp:
  *   encode      == ReedSolomon::encode      (include/ec-cpp/reed-solomon.hpp:47-81)
  *   reconstruct == ReedSolomon::reconstruct (include/ec-cpp/reed-solomon.hpp:83-134)
  *   systematic  == ReedSolomon::reconstruct_from_systematic (:143-179)
@@ -74,6 +77,34 @@ struct NPRSResult ECCR_AMD_reconstruct_batch(unsigned long n_validators, const u
                                              const uint8_t *d_present, const uint16_t *d_err_log,
                                              unsigned long batch, uint8_t *d_out,
                                              unsigned long out_stride, void *stream);
+
+/* ---- caller-owned scratch (graph capture) ---------------------------------
+ * Bytes of device scratch the batch calls above need for a shape (0 = none;
+ * also 0 for invalid parameters, which the calls themselves report), and the
+ * same calls with that scratch passed in: d_workspace 256-B aligned, at least
+ * the queried size (else UNKNOWN_* and nothing is launched).  A workspace may
+ * be shared by calls that are ordered on one stream. */
+unsigned long ECCR_AMD_encode_workspace_bytes(unsigned long n_validators,
+                                              unsigned long payload_len, unsigned long batch);
+unsigned long ECCR_AMD_error_locator_workspace_bytes(unsigned long n_validators,
+                                                     unsigned long batch);
+unsigned long ECCR_AMD_reconstruct_workspace_bytes(unsigned long n_validators,
+                                                   unsigned long shard_len, unsigned long batch);
+struct NPRSResult ECCR_AMD_encode_batch_ws(unsigned long n_validators, const uint8_t *d_payloads,
+                                           unsigned long payload_len, unsigned long payload_stride,
+                                           unsigned long batch, uint8_t *d_shards,
+                                           unsigned long shard_stride, void *d_workspace,
+                                           unsigned long workspace_bytes, void *stream);
+struct NPRSResult ECCR_AMD_error_locator_ws(unsigned long n_validators, const uint8_t *d_present,
+                                            unsigned long batch, uint16_t *d_err_log,
+                                            void *d_workspace, unsigned long workspace_bytes,
+                                            void *stream);
+/* d_pattern as in ECCR_AMD_reconstruct_batch_patterns (NULL = row b). */
+struct NPRSResult ECCR_AMD_reconstruct_batch_ws(
+    unsigned long n_validators, const uint8_t *d_shards, unsigned long shard_len,
+    unsigned long shard_stride, const uint8_t *d_present, const uint16_t *d_err_log,
+    const uint32_t *d_pattern, unsigned long batch, uint8_t *d_out, unsigned long out_stride,
+    void *d_workspace, unsigned long workspace_bytes, void *stream);
 
 /* ---- shared erasure patterns ------------------------
  * d_pattern [batch] (uint32): payload b's erasure pattern is row d_pattern[b]

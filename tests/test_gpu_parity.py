@@ -601,6 +601,88 @@ def test_host_batch_mixed_stream(oracle):
                             check_all=plen <= 100_000)
 
 
+# ------------------------------------------------------- caller-owned scratch / hipGraph
+@pytest.mark.parametrize("nv,plen,batch", [(1024, 100_003, 6), (4096, 30_001, 3), (600, 50_001, 4),
+                                           (20000, 9_001, 2)])
+def test_graph_capture_ws(oracle, nv, plen, batch):
+    """The *_ws batch calls (caller-owned scratch: no allocation, event or host
+    sync) captured into a hipGraph (torch.cuda.CUDAGraph) and replayed on new
+    inputs: encode + error locator + reconstruct, every shard and every output
+    byte vs the oracle.  One workspace serves the three calls (stream order)."""
+    import torch
+    n, k, thr = E.code_params(nv)
+    sl = E.shard_len(nv, plen)
+    ss = (sl + 63) // 64 * 64
+    need = E.workspace_bytes(nv, plen, batch)
+    assert need[1] > 0 and (nv > 4096 or need[2] > 0)  # the shapes do need scratch
+    ws = torch.empty(max(need), dtype=torch.uint8, device="cuda")
+    d_pay = torch.empty((batch, plen), dtype=torch.uint8, device="cuda")
+    d_sh = torch.full((batch, nv, ss), 0xAA, dtype=torch.uint8, device="cuda")
+    d_pr = torch.empty((batch, n), dtype=torch.uint8, device="cuda")
+    d_el = torch.empty((batch, n), dtype=torch.int16, device="cuda")
+    d_out = torch.full((batch, sl * k), 0xAA, dtype=torch.uint8, device="cuda")
+
+    def fill(seed):
+        pay = np.stack([synth.payload(seed * 100 + b, plen) for b in range(batch)])
+        cnt = thr if seed % 2 else k
+        pres = np.stack([synth.present_mask(seed * 1000 + b, nv, cnt, n) for b in range(batch)])
+        d_pay.copy_(torch.from_numpy(pay))
+        d_pr.copy_(torch.from_numpy(pres))
+        return pay, pres
+
+    def step():
+        E.encode_batch_ws(nv, d_pay, plen, plen, batch, d_sh, ss, ws)
+        E.error_locator_ws(nv, d_pr, batch, d_el, ws)
+        E.reconstruct_batch_ws(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k, ws)
+
+    fill(1)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()  # outside capture: kernel attributes, tables, fold
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    for seed in (2, 3):
+        pay, pres = fill(seed)
+        g.replay()
+        torch.cuda.synchronize()
+        sh = d_sh.cpu().numpy()
+        out = d_out.cpu().numpy()
+        for b in range(batch):
+            ref = oracle.encode(nv, pay[b].tobytes())
+            assert [sh[b, v, :sl].tobytes() for v in range(nv)] == ref, (nv, seed, b)
+            keep = [ref[v] if pres[b, v] else None for v in range(nv)]
+            assert out[b].tobytes() == oracle.reconstruct(nv, keep), (nv, seed, b)
+            assert out[b, :plen].tobytes() == pay[b].tobytes()
+
+
+def test_workspace_too_small_is_reported():
+    """A *_ws call whose workspace is below the queried size (or misaligned)
+    returns an error and launches nothing (the output stays untouched)."""
+    import torch
+    nv, plen, batch = 1024, 70_001, 3
+    n, k, thr = E.code_params(nv)
+    sl = E.shard_len(nv, plen)
+    ss = (sl + 63) // 64 * 64
+    _, wl, wr = E.workspace_bytes(nv, plen, batch)
+    d_sh = torch.zeros((batch, nv, ss), dtype=torch.uint8, device="cuda")
+    d_pr = torch.from_numpy(np.stack([synth.present_mask(b, nv, thr, n) for b in range(batch)])).cuda()
+    d_el = torch.zeros((batch, n), dtype=torch.int16, device="cuda")
+    d_out = torch.full((batch, sl * k), 0x5A, dtype=torch.uint8, device="cuda")
+    small = torch.empty(wr - 256, dtype=torch.uint8, device="cuda")
+    with pytest.raises(E.ECError) as e:
+        E.reconstruct_batch_ws(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k, small)
+    assert e.value.tag == E.Tag.UNKNOWN_RECONSTRUCTION and "workspace" in E.last_error()
+    big = torch.empty(max(wl, wr) + 512, dtype=torch.uint8, device="cuda")
+    with pytest.raises(E.ECError):  # misaligned
+        E.error_locator_ws(nv, d_pr, batch, d_el, big[1:])
+    torch.cuda.synchronize()
+    assert bool((d_out == 0x5A).all())
+
+
 # ------------------------------------------------------- runtime robustness (ADVICE r01)
 def test_scratch_failure_is_reported(oracle):
     """A shape whose per-device scratch cannot be had (here: capped below its
