@@ -224,6 +224,38 @@ struct LdsTabs {
       if (kExact || i < uint32_t(kChunks)) *reinterpret_cast<uint4 *>(base + addr(i / 5, i % 5)) = v[k];
     }
   }
+  // gather() restricted to the entries with keep(i) (cheap: no memory reads)
+  // and need(i) (may read memory: evaluated beside src(i), so it adds no
+  // dependent latency); the others are neither loaded nor written (their LDS
+  // bytes stay stale and must not be read)
+  template <int THREADS, typename F, typename K, typename N>
+  __device__ static __forceinline__ void gather_if(uint8_t *base, const MulTab *mtab, F src, K keep,
+                                                   N need, uint32_t tid) {
+    constexpr int kChunks = ENTRIES * 5;
+    constexpr int kPer = (kChunks + THREADS - 1) / THREADS;
+    constexpr bool kExact = kChunks % THREADS == 0;
+    uint32_t c[kPer];
+    bool on[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = tid + k * THREADS;
+      on[k] = (kExact || i < uint32_t(kChunks)) && keep(i / 5);
+      c[k] = on[k] ? src(i / 5) : 0u;
+      on[k] = on[k] && need(i / 5);
+    }
+    uint4 v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = tid + k * THREADS;
+      v[k] = make_uint4(0, 0, 0, 0);
+      if (on[k]) v[k] = reinterpret_cast<const uint4 *>(mtab + c[k])[i % 5];
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = tid + k * THREADS;
+      if (on[k]) *reinterpret_cast<uint4 *>(base + addr(i / 5, i % 5)) = v[k];
+    }
+  }
   // cooperative fill: entry i <- mtab[src(i)]
   template <typename F>
   __device__ static __forceinline__ void fill(uint8_t *base, const MulTab *mtab, int count,
