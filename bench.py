@@ -314,7 +314,9 @@ def main():
     total_bytes = world * B * plen * args.steps
     value = total_bytes / elapsed / 2**30
     line = {
-        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s",
+        # ranks share GPUs only in the gloo rehearsal mode (ECCR_BENCH_BACKEND)
+        "n_gpus": world if backend == "nccl" else min(world, max(torch.cuda.device_count(), 1)),
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u16",
@@ -335,6 +337,8 @@ def main():
         "reconstruct_GiBps": round(world * B * plen / ((t_loc + t_rec) * 1e-3) / 2**30, 3),
         "roundtrip_ok": ok,
     }
+    if backend != "nccl":
+        line["rehearsal"] = f"{world} ranks on {line['n_gpus']} GPU(s), gloo"
     if rank == 0 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(nv, plen, cnt, args.cpu_seconds)
     sg_failed = False
