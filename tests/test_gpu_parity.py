@@ -601,6 +601,43 @@ def test_host_batch_mixed_stream(oracle):
                             check_all=plen <= 100_000)
 
 
+@pytest.mark.parametrize("nv,lo,hi", [(4096, 0, 2048), (4096, 1024, 3072), (4096, 3000, 4096),
+                                       (3500, 0, 1500), (2048, 1024, 2048), (1500, 0, 1024),
+                                       (2500, 1024, 2048)])
+def test_batch_empty_quarters(oracle, nv, lo, hi):
+    """n = 2048 / 4096 reconstruct with every present shard in [lo, hi), so
+    whole 1024-row quarters hold no present row (clustered outages: a quarter's
+    gather is all-absent, its IFFT zero), mixed in one batch with payloads
+    whose shards span every quarter; every output byte vs the oracle."""
+    import torch
+    n, k, thr = E.code_params(nv)
+    plen, batch = 20_011, 4
+    sl = E.shard_len(nv, plen)
+    ss = (sl + 63) // 64 * 64
+    rng = np.random.default_rng(nv + lo)
+    pay = np.stack([synth.payload(31 * nv + b, plen) for b in range(batch)])
+    pres = np.zeros((batch, n), dtype=np.uint8)
+    for b in range(batch):
+        cnt = [thr, k, min(hi - lo, thr + 5), thr][b]
+        pool = np.arange(lo, min(hi, nv)) if b != 3 else np.arange(nv)
+        pres[b, rng.choice(pool, size=min(cnt, len(pool)), replace=False)] = 1
+    d_pay = torch.from_numpy(pay).cuda()
+    d_sh = torch.zeros((batch, nv, ss), dtype=torch.uint8, device="cuda")
+    d_pr = torch.from_numpy(pres).cuda()
+    d_el = torch.zeros((batch, n), dtype=torch.int16, device="cuda")
+    d_out = torch.full((batch, sl * k), 0xAA, dtype=torch.uint8, device="cuda")
+    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+    E.error_locator(nv, d_pr, batch, d_el)
+    E.reconstruct_batch(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k)
+    torch.cuda.synchronize()
+    sh = d_sh.cpu().numpy()
+    out = d_out.cpu().numpy()
+    for b in range(batch):
+        keep = [sh[b, v, :sl].tobytes() if pres[b, v] else None for v in range(nv)]
+        assert out[b].tobytes() == oracle.reconstruct(nv, keep), (nv, lo, hi, b)
+        assert out[b, :plen].tobytes() == pay[b].tobytes()
+
+
 # ------------------------------------------------------- caller-owned scratch / hipGraph
 @pytest.mark.parametrize("nv,plen,batch", [(1024, 100_003, 6), (4096, 30_001, 3), (600, 50_001, 4),
                                            (20000, 9_001, 2)])
