@@ -326,7 +326,9 @@ def workspace_bytes(nv, payload_len, batch):
 
 
 def _ws(ws):
-    return (None, 0) if ws is None else (_p(ws), ws.numel() if hasattr(ws, "numel") else ws.nbytes)
+    if ws is None:
+        return None, 0
+    return _p(ws), (ws.numel() * ws.element_size() if hasattr(ws, "numel") else ws.nbytes)
 
 
 def encode_batch_ws(nv, d_payloads, payload_len, payload_stride, batch, d_shards, shard_stride,
