@@ -228,6 +228,9 @@ def main():
     ap.add_argument("--no-scatter", action="store_true",
                     help="skip the RCCL scatter / gather phase (N > 1)")
     ap.add_argument("--scatter-timeout", type=float, default=180.0)
+    ap.add_argument("--graph", action="store_true",
+                    help="time K replays of one captured hipGraph step (ECCR_AMD_*_ws calls on "
+                         "caller-owned scratch) instead of K eager steps")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -267,33 +270,60 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     ev = []
+    # --graph: the *_ws calls on one caller-owned workspace (stream-ordered)
+    ws = (torch.empty(max(max(E.workspace_bytes(nv, plen, B)), 1), dtype=torch.uint8, device=dev)
+          if args.graph else None)
 
-    def step(record):
+    def step(record, st=None):
+        st = st or stream
         if record:
             e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-            e[0].record(stream)
-        E.encode_batch(nv, d_pay, plen, plen, B, d_sh, ss, stream)
+            e[0].record(st)
+        if ws is None:
+            E.encode_batch(nv, d_pay, plen, plen, B, d_sh, ss, st)
+        else:
+            E.encode_batch_ws(nv, d_pay, plen, plen, B, d_sh, ss, ws, st)
         if record:
-            e[1].record(stream)
-        E.error_locator(nv, d_pres, B, d_el, stream)
+            e[1].record(st)
+        if ws is None:
+            E.error_locator(nv, d_pres, B, d_el, st)
+        else:
+            E.error_locator_ws(nv, d_pres, B, d_el, ws, st)
         if record:
-            e[2].record(stream)
-        E.reconstruct_batch(nv, d_sh, sl, ss, d_pres, d_el, B, d_out, sl * k, stream)
+            e[2].record(st)
+        if ws is None:
+            E.reconstruct_batch(nv, d_sh, sl, ss, d_pres, d_el, B, d_out, sl * k, st)
+        else:
+            E.reconstruct_batch_ws(nv, d_sh, sl, ss, d_pres, d_el, B, d_out, sl * k, ws, stream=st)
         if record:
-            e[3].record(stream)
+            e[3].record(st)
             ev.append(e)
 
     for _ in range(args.warmup):
         step(False)
+    graph = None
+    if args.graph:  # one step captured after the warm-up (kernel attributes, tables set)
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step(False, torch.cuda.current_stream(dev))
+        graph.replay()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        if graph is None:
+            step(True)
+        else:
+            graph.replay()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
+    if graph is not None:  # per-kernel times from eager steps after the timed region
+        for _ in range(3):
+            step(True)
+        torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     elapsed = sharding.max_over_ranks(t1 - t0, dist, dev if backend == "nccl" else None)
@@ -337,6 +367,8 @@ def main():
         "reconstruct_GiBps": round(world * B * plen / ((t_loc + t_rec) * 1e-3) / 2**30, 3),
         "roundtrip_ok": ok,
     }
+    if graph is not None:
+        line["graph"] = "timed steps are hipGraph replays of one captured step; kernels_ms from eager steps"
     if backend != "nccl":
         line["rehearsal"] = f"{world} ranks on {line['n_gpus']} GPU(s), gloo"
     if rank == 0 and not args.no_cpu_baseline:
