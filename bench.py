@@ -36,6 +36,10 @@ import synth  # noqa: E402
 
 METRIC = "device-resident encode+reconstruct GiB/s (and % HBM roofline), n_val=1024"
 HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
+# exit status: 0 ok; 1 a round trip / scatter-gather check failed; 3 the RCCL
+# scatter / gather hung (watchdog); 4 it raised.  The JSON line is printed first
+# in every case, so the measurement is kept and marked.
+EXIT_CHECK, EXIT_SG_TIMEOUT, EXIT_SG_ERROR = 1, 3, 4
 
 
 def pmc_traffic(kernel, nv, plen, cnt, batch):
@@ -156,7 +160,8 @@ def scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out, step_s, timeou
             print(json.dumps({"scatter_gather_timeout_s": timeout_s}), file=sys.stderr, flush=True)
             if on_timeout:
                 on_timeout()  # rank 0: the measurement line, marked
-            os._exit(0)
+            # non-zero: a hung collective is a failure of a north_star component
+            os._exit(EXIT_SG_TIMEOUT)
 
     threading.Thread(target=watchdog, daemon=True).start()
     try:
@@ -374,6 +379,7 @@ def main():
     if rank == 0 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(nv, plen, cnt, args.cpu_seconds)
     sg_failed = False
+    sg_bad = False
     if dist and backend == "nccl" and not args.no_scatter:
         # the device-resident line above is the measurement; the scatter /
         # gather is reported beside it and can neither hang nor fail it
@@ -385,15 +391,18 @@ def main():
             line["scatter_gather"] = scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out,
                                                     elapsed / args.steps, args.scatter_timeout,
                                                     on_timeout)
-        except Exception as exc:  # noqa: BLE001 (reported, not raised)
+            sg_bad = not line["scatter_gather"]["ok"]
+        except Exception as exc:  # noqa: BLE001 (reported in the line, then exit 4)
             sg_failed = True
             line["scatter_gather"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist and not sg_failed:
         dist.destroy_process_group()
-    if not ok:
-        sys.exit(1)
+    if sg_failed:
+        sys.exit(EXIT_SG_ERROR)
+    if not ok or sg_bad:
+        sys.exit(EXIT_CHECK)
 
 
 if __name__ == "__main__":

@@ -147,16 +147,17 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
     ScratchLease lease(d, reconstruct_scratch_bytes(p, sl, 1), c->stream);
     if (!lease.ok()) return false;
     void *scratch = lease.ptr();
-    if (!hip_check(launch_reconstruct(p, device_tables(d), src, sl, dstride, loc->d_present,
-                                      loc->d_elog, nullptr, 1, dst, out_bytes, scratch,
-                                      c->stream),
-                   "reconstruct launch"))
-      return false;
-    // `loc` is released only after the stream has finished with it
-    return (direct || hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes,
-                                               hipMemcpyDeviceToHost, c->stream),
-                                "D2H")) &&
-           hip_check(hipStreamSynchronize(c->stream), "reconstruct");
+    const bool launched = hip_check(launch_reconstruct(p, device_tables(d), src, sl, dstride,
+                                                       loc->d_present, loc->d_elog, nullptr, 1,
+                                                       dst, out_bytes, scratch, c->stream),
+                                    "reconstruct launch");
+    const bool copied = launched && (direct || hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes,
+                                                                        hipMemcpyDeviceToHost, c->stream),
+                                                         "D2H"));
+    // `loc` is released only after the stream has finished with it (on every
+    // path: the locator cache recycles entries nobody holds)
+    const bool synced = hip_check(hipStreamSynchronize(c->stream), "reconstruct");
+    return launched && copied && synced;
   }
   return (direct || hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost,
                                              c->stream),
@@ -389,21 +390,20 @@ NPRSResult ECCR_AMD_init_device(void) {
 
 namespace {
 // Device scratch of one batch call: the caller's workspace (the *_ws entry
-// points: no allocation, no event, no host synchronisation, so the call can be
-// captured into a hipGraph once the shape has run once) or else the
-// per-device lease.  `ok` false = too small / misaligned workspace or a failed
-// allocation: nothing may be launched.
+// points) or else the scratch private to the call's stream (stream_scratch).
+// Either way, once the shape has run once on the stream, the call allocates,
+// records and waits on nothing (capturable into a hipGraph), and calls on
+// different streams never wait on each other.  `ok` false = too small /
+// misaligned workspace or a failed allocation: nothing may be launched.
 struct BatchScratch {
-  ScratchLease lease;
   void *p = nullptr;
   bool ok = false;
-  BatchScratch(DeviceState *d, size_t need, hipStream_t s, const Workspace *ws)
-      : lease(d, ws ? 0 : need, s) {
-    if (!ws) {
-      ok = lease.ok();
-      p = lease.ptr();
-    } else if (need == 0) {
+  BatchScratch(DeviceState *d, size_t need, hipStream_t s, const Workspace *ws) {
+    if (need == 0) {
       ok = true;
+    } else if (!ws) {
+      p = stream_scratch(d, s, need);
+      ok = p != nullptr;
     } else if (!ws->ptr || ws->bytes < need || reinterpret_cast<uintptr_t>(ws->ptr) % 256 != 0) {
       set_error("erasure_coding_crust(amd): workspace of " + std::to_string(ws->bytes) +
                 " bytes (256-B aligned required) is below the " + std::to_string(need) +
@@ -453,6 +453,7 @@ NPRSResult error_locator(unsigned long nv, const uint8_t *d_present, unsigned lo
     return result(NPRS_RESULT_OK);
   }
   // one locator per distinct pattern (§8f row 3), then copied to its followers
+  if (batch >= (1ul << 31)) return result(NPRS_RESULT_BAD_PAYLOAD);  // uint32 pattern indices
   const size_t pat_bytes = (batch * 4 + 255) / 256 * 256;
   BatchScratch sc(d, locator_scratch_bytes(batch), s, ws);
   if (!sc.ok) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
@@ -536,12 +537,12 @@ NPRSResult ECCR_AMD_dedup_patterns(unsigned long nv, const uint8_t *d_present, u
   CodeParams p;
   NPRSResult r = params_or_error(nv, &p);
   if (r.tag != NPRS_RESULT_OK) return r;
+  if (batch >= (1ul << 31)) return result(NPRS_RESULT_BAD_PAYLOAD);  // uint32 pattern indices
   DeviceState *d = device_state();
   if (!d) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  ScratchLease lease(d, dedup_scratch_bytes(batch), s);
-  if (!lease.ok() ||
-      !hip_check(launch_dedup_patterns(p, d_present, batch, d_pattern, lease.ptr(), s), "pattern dedup"))
+  BatchScratch sc(d, dedup_scratch_bytes(batch), s, nullptr);
+  if (!sc.ok || !hip_check(launch_dedup_patterns(p, d_present, batch, d_pattern, sc.p, s), "pattern dedup"))
     return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
   return result(NPRS_RESULT_OK);
 }

@@ -429,8 +429,8 @@ hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t 
 }
 
 namespace {
-uint32_t dedup_cap(size_t batch) {  // hash slots: a power of two >= 2 * batch
-  uint32_t c = 64;
+size_t dedup_cap(size_t batch) {  // hash slots: a power of two >= 2 * batch (batch < 2^31)
+  size_t c = 64;
   while (c < 2 * batch) c <<= 1;
   return c;
 }
@@ -444,8 +444,8 @@ size_t dedup_scratch_bytes(size_t batch) {
 hipError_t launch_dedup_patterns(const CodeParams &p, const uint8_t *d_present, size_t batch,
                                  uint32_t *d_pattern, void *scratch, hipStream_t s) {
   if (batch == 0) return hipSuccess;
-  if (!scratch) return hipErrorInvalidValue;
-  const uint32_t cap = dedup_cap(batch);
+  if (!scratch || batch >= (size_t(1) << 31)) return hipErrorInvalidValue;
+  const uint32_t cap = uint32_t(dedup_cap(batch));
   uint64_t *hash = static_cast<uint64_t *>(scratch);
   unsigned long long *keys = reinterpret_cast<unsigned long long *>(hash + batch);
   uint32_t *vals = reinterpret_cast<uint32_t *>(keys + cap);

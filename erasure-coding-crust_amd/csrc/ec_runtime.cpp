@@ -26,14 +26,23 @@ struct DeviceState {
   hipEvent_t scratch_done = nullptr;  // the last lease's work on its stream
   bool scratch_used = false;
   std::mutex loc_mu;
-  std::list<std::shared_ptr<const Locator>> loc;  // most recent first
+  std::list<std::shared_ptr<Locator>> loc;  // most recent first
   unsigned long loc_hits = 0, loc_misses = 0;
+  struct StreamBuf {
+    hipStream_t s;
+    void *p;
+    size_t cap;
+  };
+  std::mutex ss_mu;
+  std::list<StreamBuf> ss;  // per-stream scratch, most recently used first
 };
 
 namespace {
 thread_local std::string t_err;
 std::mutex g_mu;
-std::vector<std::unique_ptr<DeviceState>> g_dev;
+// never destroyed: its entries own HIP objects, and HIP calls from static
+// destructors at process exit can crash or hang; process teardown reclaims them
+std::vector<std::unique_ptr<DeviceState>> &g_dev = *new std::vector<std::unique_ptr<DeviceState>>();
 
 bool hip_ok(hipError_t e, const char *what) {
   if (e == hipSuccess) return true;
@@ -190,26 +199,47 @@ Locator::~Locator() {
 std::shared_ptr<const Locator> cached_locator(DeviceState *d, const CodeParams &p,
                                               const std::vector<uint8_t> &present,
                                               hipStream_t stream) {
-  std::lock_guard<std::mutex> lk(d->loc_mu);
-  for (auto it = d->loc.begin(); it != d->loc.end(); ++it)
-    if ((*it)->nv == p.nv && (*it)->present == present) {
-      std::shared_ptr<const Locator> hit = *it;
-      d->loc.erase(it);
-      d->loc.push_front(hit);
-      ++d->loc_hits;
-      if (!hip_ok(hipStreamWaitEvent(stream, hit->ready, 0), "locator wait")) return nullptr;
-      return hit;
+  // declared first, so destroyed last: an evicted entry still held elsewhere
+  // is freed by its last holder, never here under loc_mu
+  std::shared_ptr<Locator> evicted;
+  std::shared_ptr<Locator> L;
+  {
+    std::lock_guard<std::mutex> lk(d->loc_mu);
+    for (auto it = d->loc.begin(); it != d->loc.end(); ++it)
+      if ((*it)->nv == p.nv && (*it)->present == present) {
+        std::shared_ptr<Locator> hit = *it;
+        d->loc.erase(it);
+        d->loc.push_front(hit);
+        ++d->loc_hits;
+        if (!hip_ok(hipStreamWaitEvent(stream, hit->ready, 0), "locator wait")) return nullptr;
+        return hit;
+      }
+    ++d->loc_misses;
+    if (d->loc.size() >= kLocatorCache) {
+      evicted = std::move(d->loc.back());
+      d->loc.pop_back();
+      // nobody else holds it (no new holder can appear: it left the list under
+      // the lock), so only its own locator kernel may still touch the buffers
+      if (evicted.use_count() == 1 && evicted->cap_n >= p.n) L = std::move(evicted);
     }
-  ++d->loc_misses;
+  }
   const uint16_t *fold = device_fold(d, p.n);
   if (!fold) return nullptr;
-  auto L = std::make_shared<Locator>();
+  if (L) {
+    // its kernel (and the H2D of its key) finished long ago in practice; wait
+    // on the host, as the key below is rewritten by the host
+    if (!hip_ok(hipEventSynchronize(L->ready), "locator recycle wait")) return nullptr;
+  } else {
+    L = std::make_shared<Locator>();
+    L->cap_n = p.n;
+    if (!hip_ok(hipMalloc(&L->d_present, p.n), "hipMalloc(locator)") ||
+        !hip_ok(hipMalloc(&L->d_elog, size_t(p.n) * 2), "hipMalloc(locator)") ||
+        !hip_ok(hipEventCreateWithFlags(&L->ready, hipEventDisableTiming), "hipEventCreate"))
+      return nullptr;
+  }
   L->nv = p.nv;
   L->present = present;
-  if (!hip_ok(hipMalloc(&L->d_present, p.n), "hipMalloc(locator)") ||
-      !hip_ok(hipMalloc(&L->d_elog, size_t(p.n) * 2), "hipMalloc(locator)") ||
-      !hip_ok(hipEventCreateWithFlags(&L->ready, hipEventDisableTiming), "hipEventCreate") ||
-      !hip_ok(hipMemcpyAsync(L->d_present, L->present.data(), p.n, hipMemcpyHostToDevice, stream),
+  if (!hip_ok(hipMemcpyAsync(L->d_present, L->present.data(), p.n, hipMemcpyHostToDevice, stream),
               "H2D present") ||
       !hip_ok(launch_error_locator(p, L->d_present, 1, fold, nullptr, L->d_elog, stream),
               "error locator launch") ||
@@ -217,9 +247,46 @@ std::shared_ptr<const Locator> cached_locator(DeviceState *d, const CodeParams &
     (void)hipStreamSynchronize(stream);  // nothing issued above may outlive L
     return nullptr;
   }
+  std::lock_guard<std::mutex> lk(d->loc_mu);
   d->loc.push_front(L);
-  if (d->loc.size() > kLocatorCache) d->loc.pop_back();  // freed once its last user is done
   return L;
+}
+
+void *stream_scratch(DeviceState *d, hipStream_t s, size_t bytes) {
+  if (bytes == 0) return nullptr;
+  const size_t limit = g_scratch_limit;
+  if (limit && bytes > limit) {  // as if hipMalloc had failed
+    set_error("erasure_coding_crust(amd): scratch of " + std::to_string(bytes) +
+              " bytes exceeds the limit set by ECCR_AMD_set_scratch_limit");
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lk(d->ss_mu);
+  auto it = d->ss.begin();
+  while (it != d->ss.end() && it->s != s) ++it;
+  if (it != d->ss.end()) {
+    d->ss.splice(d->ss.begin(), d->ss, it);  // most recent first
+    DeviceState::StreamBuf &b = d->ss.front();
+    if (b.cap >= bytes) return b.p;
+    // grow: this stream's earlier work may still read the smaller buffer
+    if (!hip_ok(hipStreamSynchronize(s), "scratch grow sync")) return nullptr;
+    (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    if (!hip_ok(hipMalloc(&b.p, bytes), "hipMalloc(stream scratch)")) return nullptr;
+    b.cap = bytes;
+    return b.p;
+  }
+  if (d->ss.size() >= kStreamScratch) {
+    // the oldest entry's stream may be gone (its handle dangling): wait for
+    // the whole device instead of that stream, then release it (rare)
+    if (!hip_ok(hipDeviceSynchronize(), "scratch evict sync")) return nullptr;
+    (void)hipFree(d->ss.back().p);
+    d->ss.pop_back();
+  }
+  void *p = nullptr;
+  if (!hip_ok(hipMalloc(&p, bytes), "hipMalloc(stream scratch)")) return nullptr;
+  d->ss.push_front({s, p, bytes});
+  return p;
 }
 
 void locator_cache_stats(DeviceState *d, unsigned long *hits, unsigned long *misses) {

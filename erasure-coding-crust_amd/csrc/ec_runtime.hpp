@@ -48,6 +48,17 @@ class ScratchLease {
   bool held_ = false;
 };
 
+// Scratch private to one (device, stream), for the batch calls made without a
+// caller workspace: grown on the first call of a larger shape on that stream
+// (which synchronises the stream before the smaller buffer is freed);
+// afterwards a call allocates, records and waits on nothing, so it can be
+// captured into a hipGraph, and calls on different streams never wait on each
+// other.  At most kStreamScratch streams per device keep a buffer (the least
+// recently used beyond that is released after a device synchronisation).
+// nullptr (error set) if the allocation failed or exceeds the scratch limit.
+constexpr size_t kStreamScratch = 64;
+void *stream_scratch(DeviceState *d, hipStream_t s, size_t bytes);
+
 // Per-pattern erasure-locator cache of the per-call C ABI (SURVEY.md §8f
 // row 3): the locator of a pattern (n_validators + present bitmap) is computed
 // once per device and reused while it is among the most recent kLocatorCache
@@ -55,14 +66,19 @@ class ScratchLease {
 constexpr size_t kLocatorCache = 64;
 struct Locator {
   uint32_t nv = 0;
+  uint32_t cap_n = 0;            // n the device buffers were sized for (recycled on eviction)
   std::vector<uint8_t> present;  // the key: [n] flags
   uint8_t *d_present = nullptr;  // [n] on the device
   uint16_t *d_elog = nullptr;    // [n] log-domain multipliers (ECCR_AMD_error_locator)
   hipEvent_t ready = nullptr;    // recorded after the locator kernel
-  ~Locator();                    // waits for `ready`, then frees
+  ~Locator();                    // waits for `ready`, then frees (never under the cache lock)
 };
 // The pattern's locator, computed on `stream` on a miss; on a hit `stream`
 // is ordered after the kernel that computed it.  nullptr on a HIP error.
+// Holders synchronise their stream before dropping the pointer (every C-ABI
+// call does), so an evicted entry nobody holds is idle apart from its own
+// locator kernel: a miss recycles its buffers and event (ordered after that
+// kernel) instead of freeing and allocating.
 std::shared_ptr<const Locator> cached_locator(DeviceState *d, const CodeParams &p,
                                               const std::vector<uint8_t> &present,
                                               hipStream_t stream);

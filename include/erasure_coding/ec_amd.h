@@ -4,18 +4,19 @@
  *
  * All pointers named d_* are device pointers on the codec's device; `stream`
  * is a hipStream_t (NULL = the legacy default stream).  Calls are asynchronous
- * on `stream` and the caller owns every buffer it passes.  The plain calls
- * are NOT graph-capture-safe in general: shapes that need device scratch
- * (k = 1024 encodes, the fast reconstructs' per-payload gather order (4 n
- * bytes per payload), n > 4096 generic kernels, ECCR_AMD_error_locator /
- * ECCR_AMD_dedup_patterns with batch > 1) take a per-device scratch buffer
- * that may be (re)allocated with hipMalloc / hipFree and is ordered across
- * streams with an event (hipStreamWaitEvent, and hipEventSynchronize when it
- * grows).  The *_ws variants take caller-owned scratch instead (size from the
- * matching *_workspace_bytes query) and then allocate, record and wait on
- * nothing: after one call of a shape outside capture (the first call per
- * (device, kernel) sets a kernel attribute and uploads the tables) they can be
- * captured into a hipGraph and replayed.  Results are bit-exact with ec-cpp:
+ * on `stream` and the caller owns every buffer it passes.  Shapes that need
+ * device scratch (k = 1024 encodes, the fast reconstructs' per-payload gather
+ * order (4 n bytes per payload), n > 4096 generic kernels,
+ * ECCR_AMD_error_locator / ECCR_AMD_dedup_patterns with batch > 1) use, in the
+ * plain calls, a scratch buffer private to (device, stream): the first call of
+ * a larger shape on a stream allocates it (hipMalloc, after synchronising that
+ * stream if a smaller one is replaced); afterwards the plain calls allocate,
+ * record and wait on nothing, and calls on different streams never wait on
+ * each other.  The *_ws variants take caller-owned scratch instead (size from
+ * the matching *_workspace_bytes query) and never allocate.  Either form can
+ * be captured into a hipGraph and replayed once the shape has run once on the
+ * stream outside capture (the first call per (device, kernel) also sets a
+ * kernel attribute and uploads the tables).  Results are bit-exact with ec-cpp:
  *   encode      == ReedSolomon::encode      (include/ec-cpp/reed-solomon.hpp:47-81)
  *   reconstruct == ReedSolomon::reconstruct (include/ec-cpp/reed-solomon.hpp:83-134)
  *   systematic  == ReedSolomon::reconstruct_from_systematic (:143-179)
@@ -112,8 +113,11 @@ struct NPRSResult ECCR_AMD_reconstruct_batch_ws(
  * NULL = row b).  The usual case: the same validators missing for every block,
  * i.e. ONE present row and ONE locator for the whole batch. */
 
-/* d_pattern[b] = the smallest index whose pattern (present flags of positions
- * < n_validators) equals payload b's, over the rows of d_present [batch][n]. */
+/* d_pattern[b] = a row whose pattern (present flags of positions < n_validators)
+ * equals payload b's and which is its own leader (d_pattern[l] == l), or b
+ * itself; normally the smallest such index (a 64-bit hash collision between
+ * different patterns only costs the sharing: each row then leads itself).
+ * batch < 2^31 (else BAD_PAYLOAD, nothing launched). */
 struct NPRSResult ECCR_AMD_dedup_patterns(unsigned long n_validators, const uint8_t *d_present,
                                           unsigned long batch, uint32_t *d_pattern, void *stream);
 
@@ -172,8 +176,8 @@ struct NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long n_validators,
                                                   unsigned long batch, uint8_t *h_out,
                                                   unsigned long out_stride, unsigned long chunk);
 
-/* Cap on one per-device scratch allocation in bytes (0 = no cap, the
- * default).  A call whose shape needs more fails with UNKNOWN_CODE_PARAM
+/* Cap on one scratch allocation in bytes (per device or per stream; 0 = no
+ * cap, the default).  A call whose shape needs more fails with UNKNOWN_CODE_PARAM
  * (encode) / UNKNOWN_RECONSTRUCTION (reconstruct) exactly as when hipMalloc
  * runs out of memory; nothing is launched.  Applies to the per-call C ABI
  * and the device-batch calls; the host-batch pipeline's slots own their

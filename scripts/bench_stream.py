@@ -13,7 +13,9 @@ chunk = 0).  Whole-job rate = stream bytes / max-over-ranks time.
   python scripts/bench_stream.py                      # 1 GPU
   python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
       scripts/bench_stream.py                         # 8 GPUs
-Prints one JSON line on rank 0.
+ECCR_BENCH_BACKEND=gloo (rehearsal only, as bench.py): ranks may share a GPU,
+the barrier / max timing run on CPU tensors over gloo.
+Prints one JSON line on rank 0; exit status 1 if a round trip failed.
 """
 from __future__ import annotations
 
@@ -45,12 +47,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("ECCR_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # collective tensors
     assert E.lib().ECCR_AMD_init_device().tag == 0, E.last_error()
     nv = a.nv
     n, k, thr = E.code_params(nv)
@@ -94,19 +103,22 @@ def main():
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
-    el = sharding.max_over_ranks(t1 - t0, dist, dev)
+    el = sharding.max_over_ranks(t1 - t0, dist, cdev)
     ok = all(torch.equal(out[:, :plen], pay) for plen, B, sl, pay, sh, comp, idx_t, out in work)
     if dist:
-        f = torch.tensor([int(ok)], dtype=torch.int32, device=dev)
+        f = torch.tensor([int(ok)], dtype=torch.int32, device=cdev)
         dist.all_reduce(f, op=dist.ReduceOp.MIN)
         ok = bool(f.item())
     total = sum(sizes) * a.reps
     line = {"metric": "config5 mixed-size stream, end-to-end host->device->host encode + reconstruct",
-            "value": round(total / el / 2**30, 3), "unit": "GiB/s", "n_gpus": world,
+            "value": round(total / el / 2**30, 3), "unit": "GiB/s",
+            "n_gpus": world if backend == "nccl" else min(world, max(torch.cuda.device_count(), 1)),
             "n_validators": nv, "stream_payloads": len(sizes), "stream_bytes": sum(sizes),
             "sizes": README_SIZES, "reps": a.reps, "seconds": round(el, 4),
             "present_shards": thr, "my_payloads": len(mine), "roundtrip_ok": ok,
             "partition": "sharding.balanced_partition (bytes, greedy LPT)"}
+    if backend != "nccl":
+        line["rehearsal"] = f"{world} ranks on {line['n_gpus']} GPU(s), {backend}"
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:

@@ -142,7 +142,8 @@ def main():
             (4096, 5000, {"count": "k", "seed": 10**6 + 4}),
             (65536, 1, {"count": "k", "seed": 10**6 + 5}),
             (65536, 70_000, {"count": "threshold", "seed": 10**6 + 6}),
-            (1024, 10_000_000, {"count": "threshold", "seed": 10**6 + 7})):  # config 3
+            (1024, 10_000_000, {"count": "threshold", "seed": 10**6 + 7}),   # config 3
+            (1024, 10_000_000, {"count": "k", "seed": 10**6 + 9})):          # config 3: k random shards
         cases.append({"nv": nv, "payload": {"kind": "splitmix", "seed": 7000 + plen % 997, "len": plen},
                       "present": pres, "tag": "config"})
     cases.append({"nv": 1024, "payload": {"kind": "mod255", "len": 1_000_000},

@@ -193,6 +193,68 @@ def test_batch_config2_roundtrip():
     assert b"".join(single) == sh[3].tobytes()
 
 
+def test_batch_config3_k_golden(oracle, golden_vectors):
+    """BASELINE config 3 read as 'reconstruct from k random shards' (10 MB,
+    n_validators = 1024, c = k = 256) on the device batch path, B = 2: payload 0
+    is the golden case generated by the reference ec-cpp (tests/golden, tag
+    config, count k), payload 1 is checked against the oracle."""
+    import torch
+    case = next(c for c in golden_vectors if c["tag"] == "config" and c["nv"] == 1024
+                and c["payload_len"] == 10_000_000 and c["present"]["count"] == "k")
+    nv, plen, batch = 1024, 10_000_000, 2
+    n, k, thr = E.code_params(nv)
+    sl = E.shard_len(nv, plen)
+    ss = (sl + 63) // 64 * 64
+    pay = np.stack([np.frombuffer(payload_from_spec(case["payload"]), np.uint8),
+                    synth.payload(4242, plen)])
+    pres = np.zeros((batch, n), dtype=np.uint8)
+    pres[0, present_from_spec(nv, k, thr, case["present"])] = 1
+    pres[1, synth.present_set(4243, nv, k)] = 1
+    assert (pres.sum(axis=1) == k).all()
+    d_pay = torch.from_numpy(pay).cuda()
+    d_sh = _prefilled((batch, nv, ss))
+    d_pr = torch.from_numpy(pres).cuda()
+    d_el = torch.zeros((batch, n), dtype=torch.int16, device="cuda")
+    d_out = _prefilled((batch, sl * k))
+    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+    torch.cuda.synchronize()
+    for b in range(batch):  # absent rows: garbage that must never be read
+        gone = np.where(pres[b][:nv] == 0)[0]
+        d_sh[b, torch.from_numpy(gone).cuda()] = 0x5C
+    E.error_locator(nv, d_pr, batch, d_el)
+    E.reconstruct_batch(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k)
+    torch.cuda.synchronize()
+    sh = d_sh.cpu().numpy()
+    out = d_out.cpu().numpy()
+    assert sha(out[0].tobytes()) == case["reconstructed_sha256"]
+    ref1 = oracle.encode(nv, pay[1].tobytes())
+    keep = [ref1[i] if pres[1][i] else None for i in range(nv)]
+    assert out[1].tobytes() == oracle.reconstruct(nv, keep)
+    assert out[1][:plen].tobytes() == pay[1].tobytes()
+    # the encode of payload 0 (present rows survive the 0x5C overwrite) vs golden
+    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+    torch.cuda.synchronize()
+    sh = d_sh.cpu().numpy()
+    assert sha(np.ascontiguousarray(sh[0][:, :sl]).tobytes()) == case["shards_sha256"]
+    assert [sh[1][v, :sl].tobytes() for v in range(nv)] == ref1
+
+
+def test_batch_nv4096_1MB(oracle):
+    """BASELINE config 4 shape at full payload size on the device batch path:
+    n_validators = 4096 (n = 4096, k = 1024), 1 MB payloads, B = 4, so several
+    k = 1024 encode tiles span payloads and the four encode_k1024 launches share
+    one coefficient scratch; every shard and output byte vs the oracle."""
+    nv, plen, batch = 4096, 1_000_000, 4
+    pay, pres, sh, el, out = _batch_case(nv, plen, batch, seed0=40960, pad=64)
+    n, k, _ = E.code_params(nv)
+    for b in range(batch):
+        ref = oracle.encode(nv, pay[b].tobytes())
+        assert b"".join(ref) == sh[b].tobytes(), b
+        keep = [ref[i] if pres[b][i] else None for i in range(nv)]
+        assert out[b].tobytes() == oracle.reconstruct(nv, keep), b
+        assert out[b][:plen].tobytes() == pay[b].tobytes(), b
+
+
 def test_batch_systematic():
     import torch
     nv, plen, batch = 1024, 100_000, 3
@@ -479,6 +541,33 @@ def test_shared_patterns(oracle, nv, plen, pad):
         assert out[b].tobytes() == oracle.reconstruct(nv, keep), b
 
 
+def test_locator_cache_eviction(oracle):
+    """More distinct patterns than the per-call locator cache holds (64): every
+    miss past the cap recycles the least recent entry's device buffers; results
+    stay bit-exact, a re-used recent pattern hits, an evicted one misses."""
+    import time
+    nv, plen = 1024, 3000
+    n, k, thr = E.code_params(nv)
+    p = synth.payload(99, plen).tobytes()
+    sh = E.obtain_chunks(nv, p)
+    sets = [set(int(x) for x in synth.present_set(50_000 + j, nv, thr)) for j in range(80)]
+    h0, m0 = E.locator_cache_stats()
+    t0 = time.perf_counter()
+    for j, keep in enumerate(sets):
+        out = decode_subset(nv, sh, keep)
+        if j % 9 == 0 or j >= 70:
+            assert out == oracle.reconstruct(nv, [sh[i] if i in keep else None for i in range(nv)]), j
+        assert out[:plen] == p
+    per_miss_ms = (time.perf_counter() - t0) / len(sets) * 1e3
+    h1, m1 = E.locator_cache_stats()
+    assert (h1 - h0, m1 - m0) == (0, 80)
+    assert decode_subset(nv, sh, sets[79])[:plen] == p  # recent: hit
+    assert decode_subset(nv, sh, sets[0])[:plen] == p   # evicted: miss
+    h2, m2 = E.locator_cache_stats()
+    assert (h2 - h1, m2 - m1) == (1, 1)
+    print(f"per-call reconstruct with a locator miss: {per_miss_ms:.3f} ms")
+
+
 def test_locator_cache_per_call(oracle):
     """ECCR_reconstruct computes a pattern's locator once per device and then
     reuses it (the same validators missing for every block)."""
@@ -639,13 +728,16 @@ def test_batch_empty_quarters(oracle, nv, lo, hi):
 
 
 # ------------------------------------------------------- caller-owned scratch / hipGraph
+@pytest.mark.parametrize("use_ws", [True, False])
 @pytest.mark.parametrize("nv,plen,batch", [(1024, 100_003, 6), (4096, 30_001, 3), (600, 50_001, 4),
                                            (20000, 9_001, 2)])
-def test_graph_capture_ws(oracle, nv, plen, batch):
-    """The *_ws batch calls (caller-owned scratch: no allocation, event or host
-    sync) captured into a hipGraph (torch.cuda.CUDAGraph) and replayed on new
-    inputs: encode + error locator + reconstruct, every shard and every output
-    byte vs the oracle.  One workspace serves the three calls (stream order)."""
+def test_graph_capture_ws(oracle, nv, plen, batch, use_ws):
+    """The batch calls captured into a hipGraph (torch.cuda.CUDAGraph) and
+    replayed on new inputs: encode + error locator + reconstruct, every shard
+    and every output byte vs the oracle.  use_ws: the *_ws calls on one
+    caller-owned workspace (stream order); else the plain calls, whose scratch
+    is private to the stream they were warmed up on (no allocation, event or
+    host sync once warm: ec_amd.h)."""
     import torch
     n, k, thr = E.code_params(nv)
     sl = E.shard_len(nv, plen)
@@ -668,19 +760,24 @@ def test_graph_capture_ws(oracle, nv, plen, batch):
         return pay, pres
 
     def step():
-        E.encode_batch_ws(nv, d_pay, plen, plen, batch, d_sh, ss, ws)
-        E.error_locator_ws(nv, d_pr, batch, d_el, ws)
-        E.reconstruct_batch_ws(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k, ws)
+        if use_ws:
+            E.encode_batch_ws(nv, d_pay, plen, plen, batch, d_sh, ss, ws)
+            E.error_locator_ws(nv, d_pr, batch, d_el, ws)
+            E.reconstruct_batch_ws(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k, ws)
+        else:
+            E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+            E.error_locator(nv, d_pr, batch, d_el)
+            E.reconstruct_batch(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k)
 
     fill(1)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
-        step()  # outside capture: kernel attributes, tables, fold
+        step()  # outside capture: kernel attributes, tables, fold, the stream's scratch
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, stream=s):
         step()
     for seed in (2, 3):
         pay, pres = fill(seed)

@@ -1,0 +1,52 @@
+"""The multi-process HIP path under test: bench.py and the
+config-5 stream driver launched by torchrun with 2 ranks that share the one
+GPU of the box (gloo carries the barrier / max timing: ECCR_BENCH_BACKEND),
+each rank running the HIP library on its own payload range.  The children are
+fresh processes started before they make any GPU call; their round trips must
+hold and they must exit 0.  The RCCL runs on one rank per GPU are the
+driver's (SCALE_rNN), which this rehearses process for process."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _torchrun(script_args, timeout=300):
+    env = dict(os.environ)
+    env["ECCR_BENCH_BACKEND"] = "gloo"
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + script_args
+    r = subprocess.run(["timeout", "-k", "10", str(timeout)] + cmd, cwd=ROOT, env=env,
+                       capture_output=True, text=True)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    return r, (json.loads(lines[-1]) if lines else None)
+
+
+def test_bench_two_ranks_share_gpu():
+    r, line = _torchrun(["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+                         "--batch", "48", "--payload", "100000", "--no-cpu-baseline"])
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert line is not None and line["roundtrip_ok"], line
+    assert line["config"]["parallelism"] == "dp2" and "gloo" in line["rehearsal"]
+    assert line["value"] > 0 and line["steps"] == 2
+
+
+def test_bench_stream_two_ranks_share_gpu():
+    r, line = _torchrun([os.path.join("scripts", "bench_stream.py"), "--per-size", "2", "--reps", "1"])
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert line is not None and line["roundtrip_ok"], line
+    assert line["my_payloads"] >= 1 and "gloo" in line["rehearsal"]

@@ -204,3 +204,40 @@ def test_bench_scatter_gather_gloo():
     assert all(p.exitcode == 0 for p in procs)
     assert r["ok"] and r["scatter_bytes"] == 3 * 1001 and r["gather_bytes"] == 3 * 1024
 
+
+
+def _bench_sg_hang_worker(rank, world, port):
+    """rank 0 enters bench.scatter_gather, rank 1 never joins the collective:
+    the watchdog must end rank 0 with the timeout status (bench.EXIT_SG_TIMEOUT),
+    not 0, after printing the marked line."""
+    import time
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if rank == 1:
+        time.sleep(20)
+        os._exit(0)
+    B, plen = 2, 101
+    dev = torch.device("cpu")
+    d_pay = torch.zeros((B, plen), dtype=torch.uint8)
+    bench.scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_pay.clone(), 1e-3, 3.0,
+                         lambda: print('{"marked": true}', flush=True))
+    os._exit(0)  # not reached: the watchdog exits first
+
+
+def test_bench_scatter_gather_timeout_exits_nonzero():
+    import torch.multiprocessing as mp
+    sys.path.insert(0, ROOT)
+    import bench
+    ctx = mp.get_context("spawn")
+    world, port = 2, _free_port()
+    procs = [ctx.Process(target=_bench_sg_hang_worker, args=(r, world, port)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert procs[0].exitcode == bench.EXIT_SG_TIMEOUT == 3
