@@ -415,8 +415,11 @@ struct BatchScratch {
   }
 };
 
-size_t locator_scratch_bytes(size_t batch) {
-  return batch <= 1 ? 0 : (batch * 4 + 255) / 256 * 256 + dedup_scratch_bytes(batch);
+// batch > 1 deduplicates patterns only where a locator is expensive (n > 4096:
+// the workgroup form); below, every row is computed by the wave form (ec_kernels)
+size_t locator_scratch_bytes(const CodeParams &p, size_t batch) {
+  return batch <= 1 || locator_wave_applicable(p.n) ? 0
+                                                     : (batch * 4 + 255) / 256 * 256 + dedup_scratch_bytes(batch);
 }
 
 NPRSResult encode_batch(unsigned long nv, const uint8_t *d_payloads, unsigned long plen,
@@ -446,7 +449,7 @@ NPRSResult error_locator(unsigned long nv, const uint8_t *d_present, unsigned lo
   DeviceState *d = device_state();
   const uint16_t *fold = d ? device_fold(d, p.n) : nullptr;
   if (!fold) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-  if (batch <= 1) {
+  if (batch <= 1 || locator_wave_applicable(p.n)) {
     if (!hip_check(launch_error_locator(p, d_present, batch, fold, nullptr, d_err_log, s),
                    "error locator launch"))
       return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
@@ -455,7 +458,7 @@ NPRSResult error_locator(unsigned long nv, const uint8_t *d_present, unsigned lo
   // one locator per distinct pattern (§8f row 3), then copied to its followers
   if (batch >= (1ul << 31)) return result(NPRS_RESULT_BAD_PAYLOAD);  // uint32 pattern indices
   const size_t pat_bytes = (batch * 4 + 255) / 256 * 256;
-  BatchScratch sc(d, locator_scratch_bytes(batch), s, ws);
+  BatchScratch sc(d, locator_scratch_bytes(p, batch), s, ws);
   if (!sc.ok) return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
   uint32_t *pat = static_cast<uint32_t *>(sc.p);
   void *work = static_cast<uint8_t *>(sc.p) + pat_bytes;
@@ -522,7 +525,7 @@ NPRSResult ECCR_AMD_error_locator(unsigned long nv, const uint8_t *d_present, un
 unsigned long ECCR_AMD_error_locator_workspace_bytes(unsigned long nv, unsigned long batch) {
   CodeParams p;
   if (code_params(nv, &p) != ParamError::kOk) return 0;
-  return locator_scratch_bytes(batch);
+  return locator_scratch_bytes(p, batch);
 }
 
 NPRSResult ECCR_AMD_error_locator_ws(unsigned long nv, const uint8_t *d_present,

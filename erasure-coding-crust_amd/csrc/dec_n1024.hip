@@ -178,6 +178,27 @@ __device__ __forceinline__ void swap_bit(uint32_t &x, uint32_t &y, int b, bool h
 
 __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ? 0u : c; }
 
+// 8 shard bytes at any even address, zero past `avail` (bytes valid from p):
+// aligned dwords that each hold at least one wanted byte, funnel-shifted
+__device__ __forceinline__ uint2 load8_any(const uint8_t *p, uint32_t avail) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  if (avail >= 8 && (a & 7) == 0) return *reinterpret_cast<const uint2 *>(p);
+  if (avail == 0) return make_uint2(0, 0);
+  const uint32_t sh = uint32_t(a & 3), nb = avail < 8 ? avail : 8u;
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+  uint32_t d[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) d[i] = uint32_t(4 * i) < sh + nb ? q[i] : 0u;
+  uint32_t w[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+    const uint32_t have = nb > uint32_t(4 * j) ? nb - uint32_t(4 * j) : 0u;
+    if (have < 4) w[j] &= (1u << (8 * have)) - 1u;
+  }
+  return make_uint2(w[0], w[1]);
+}
+
 // The two waves of a SIMD (w, w + 4) take turns at the higher issue priority
 // (pass A: w + 4, pass B: w, pass C to the FFT: w + 4, output: equal), so
 // neither runs far ahead and then idles at the tile barrier while the other
@@ -244,11 +265,21 @@ hipError_t launch_gather_order(const CodeParams &p, const uint8_t *d_present,
 
 size_t gather_order_bytes(const CodeParams &p, size_t batch) { return batch * p.n * sizeof(uint32_t); }
 
+// PACKED (payloads of fewer than 32 columns, or shard pitches the 16-B row
+// loads cannot take): tiles run over the flattened column space, payload b
+// owning columns [b * ncols4, b * ncols4 + ncols) with ncols4 = columns rounded
+// up to 4, so each byte-planar group (one wave's codewords) belongs to one
+// payload; the 8 groups of a tile may belong to 8 payloads.  The gather then
+// reads each (row, group) with that payload's flag and E[v] (natural row
+// order: no gather order), and the output goes to the wave's payload.  4096
+// one-column payloads are 512 tiles instead of 4096.
+template <bool PACKED>
 __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
     const uint32_t *__restrict__ pattern, const uint32_t *__restrict__ order,
-    uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t batch, DevTables t) {
+    uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t batch, uint32_t ncols4,
+    DevTables t) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
   uint8_t *regions = lds + TAB_REGION;
@@ -264,7 +295,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
 
   const uint64_t ncols = slen / 2;
   const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);
-  const uint64_t total = uint64_t(tiles_pp) * batch;
+  const uint64_t total = PACKED ? (uint64_t(ncols4) * batch + COLS - 1) / COLS : uint64_t(tiles_pp) * batch;
   // m[0], m[1]: this thread's two gather slots (gather_order): row << 16 |
   // mul_index(E[row]), low half 0xFFFF = absent.  Loaded one tile ahead so the
   // gather's table loads wait on one global latency instead of two.
@@ -272,9 +303,18 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   // each: 0xFFFF = present (copied from the staged row), else mul_index(E[y]) (the
   // erased value is scaled by E[y]; y < 256 < nv always holds for n = 1024).
   auto load_meta = [&](uint64_t tl, uint32_t tid, uint32_t (&m)[4]) {
-    const uint64_t bb = tl / tiles_pp, pt = pattern ? pattern[bb] : bb;
+    uint64_t bb;
+    if constexpr (PACKED) {  // the payload of this wave's group (phase 5 only)
+      bb = (uint32_t(tl) * COLS + 4 * (tid >> 6)) / ncols4;
+      if (bb >= batch) bb = 0;  // no output is written for it
+    } else {
+      bb = tl / tiles_pp;
+    }
+    const uint64_t pt = pattern ? pattern[bb] : bb;
+    if constexpr (!PACKED) {
 #pragma unroll
-    for (int half = 0; half < 2; ++half) m[half] = order[bb * N + half * THREADS + tid];
+      for (int half = 0; half < 2; ++half) m[half] = order[bb * N + half * THREADS + tid];
+    }
     const uint32_t y0 = 4 * (tid & 63);
     const uint32_t p4 = *reinterpret_cast<const uint32_t *>(present + pt * N + y0);
     const uint2 e4 = *reinterpret_cast<const uint2 *>(elog + pt * N + y0);
@@ -295,11 +335,46 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     uint32_t tid = tid0;
     asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63;
-    const uint64_t b = tile / tiles_pp;
-    const uint64_t col0 = (tile % tiles_pp) * COLS;
+    uint64_t b, col0;
+    if constexpr (PACKED) {  // this wave's group: columns [col0, col0 + 4) of payload b
+      const uint32_t gw = uint32_t(tile) * COLS + 4 * (tid >> 6);
+      b = gw / ncols4;
+      col0 = uint64_t(gw % ncols4) - 4 * uint64_t(tid >> 6);  // cbase below = col0 + 4 * wave (mod 2^64)
+    } else {
+      b = tile / tiles_pp;
+      col0 = (tile % tiles_pp) * COLS;
+    }
     const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
     uint8_t *O = out + b * ostride;
 
+    if constexpr (PACKED) {
+      // ---- phase 1, packed: rows v = tid and tid + 512 (natural order), each
+      // with the 8 groups' own payloads: flag, E[v], 8 bytes (decode_main:174-177)
+      lds_barrier();  // previous tile's readers of the regions are done (LDS only)
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const uint32_t v = tid + half * THREADS;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          const uint32_t gg = uint32_t(tile) * COLS + 4 * g, bg = gg / ncols4, cg = gg % ncols4;
+          uint32_t l = 0, h = 0;
+          if (bg < batch && int(v) < nv) {
+            const uint64_t pt = pattern ? pattern[bg] : bg;
+            if (present[pt * N + v]) {
+              Tab T;
+              load_tab(t.mtab, mul_index(elog[pt * N + v]), T);
+              const uint64_t have = ncols - cg;  // columns of the group inside the payload
+              const uint2 d = load8_any(shards + uint64_t(bg) * nv * sstride + uint64_t(v) * sstride + 2 * cg,
+                                        have >= 4 ? 8u : uint32_t(2 * have));
+              if (v < uint32_t(K)) *reinterpret_cast<uint2 *>(stage + stage_addr(v, g)) = d;
+              const uint32_t xh = vperm(d.y, d.x, 0x06040200u), xl = vperm(d.y, d.x, 0x07050301u);
+              mul_acc(xl, xh, T, l, h);
+            }
+          }
+          *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l, h);
+        }
+      }
+    } else {
     // ---- phase 1: gather + scale this thread's two slots' rows (present rows
     // first, gather_order; decode_main:174-177); absent rows are written as 0.
     // The first slot's row and E[v] table are requested before the barrier
@@ -356,6 +431,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
 #pragma unroll
       for (int g = 0; g < 8; ++g)
         *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l[g], h[g]);
+    }
     }
     if (tile + gridDim.x < total) load_meta(tile + gridDim.x, tid, meta_next);
     STAMP(2);
@@ -607,7 +683,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const uint64_t col = cbase + c;
-        if (col >= ncols) break;
+        if (col >= ncols || (PACKED && b >= batch)) break;
         const uint32_t w0 = vperm(ol[0], oh[0], 0x0c0c0400u + 0x0101u * c) |
                             (vperm(ol[1], oh[1], 0x0c0c0400u + 0x0101u * c) << 16);
         const uint32_t w1 = vperm(ol[2], oh[2], 0x0c0c0400u + 0x0101u * c) |
@@ -627,6 +703,12 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
 
 bool n1024_applicable(const CodeParams &p) { return p.n == 1024 && p.k == 256; }
 
+// packed tiles: fewer columns per payload than a tile, or a shard pitch / base
+// the 16-B row loads cannot take (any even pitch and base then)
+bool n1024_packed(size_t slen, uintptr_t sh, size_t sstride) {
+  return slen / 2 < size_t(COLS) || sh % 16 != 0 || sstride % 16 != 0;
+}
+
 hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
                                     const uint8_t *d_shards, size_t slen, size_t sstride,
                                     const uint8_t *d_present, const uint16_t *d_err_log,
@@ -634,20 +716,32 @@ hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
                                     size_t batch, uint8_t *d_out, size_t ostride, void *scratch,
                                     hipStream_t s) {
   int cus = 0;
-  if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&reconstruct_n1024),
-                                          LDS_BYTES, &cus);
-      e != hipSuccess)
-    return e;
-  if (!scratch) return hipErrorInvalidValue;
-  uint32_t *order = static_cast<uint32_t *>(scratch);  // gather_order_bytes(p, batch)
-  if (const hipError_t e = launch_gather_order(p, d_present, d_err_log, d_pattern, batch, order, s);
-      e != hipSuccess)
-    return e;
-  const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
+  const bool packed = n1024_packed(slen, reinterpret_cast<uintptr_t>(d_shards), sstride);
+  const size_t ncols4 = (slen / 2 + 3) / 4 * 4;
+  if (packed && (reinterpret_cast<uintptr_t>(d_shards) % 2 != 0 || sstride % 2 != 0 ||
+                 ncols4 * batch + COLS >= (size_t(1) << 32)))
+    return hipErrorInvalidValue;
+  const void *fn = packed ? reinterpret_cast<const void *>(&reconstruct_n1024<true>)
+                          : reinterpret_cast<const void *>(&reconstruct_n1024<false>);
+  if (const hipError_t e = prepare_kernel(fn, LDS_BYTES, &cus); e != hipSuccess) return e;
+  uint32_t *order = nullptr;
+  if (!packed) {  // the packed gather reads rows in natural order
+    if (!scratch) return hipErrorInvalidValue;
+    order = static_cast<uint32_t *>(scratch);  // gather_order_bytes(p, batch)
+    if (const hipError_t e = launch_gather_order(p, d_present, d_err_log, d_pattern, batch, order, s);
+        e != hipSuccess)
+      return e;
+  }
+  const size_t tiles = packed ? (ncols4 * batch + COLS - 1) / COLS : (slen / 2 + COLS - 1) / COLS * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
-  hipLaunchKernelGGL(reconstruct_n1024, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
-                     uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, order,
-                     d_out, uint64_t(ostride), int(p.nv), uint32_t(batch), t);
+  if (packed)
+    hipLaunchKernelGGL(reconstruct_n1024<true>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
+                       uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, order,
+                       d_out, uint64_t(ostride), int(p.nv), uint32_t(batch), uint32_t(ncols4), t);
+  else
+    hipLaunchKernelGGL(reconstruct_n1024<false>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,
+                       uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, order,
+                       d_out, uint64_t(ostride), int(p.nv), uint32_t(batch), uint32_t(ncols4), t);
   return hipGetLastError();
 }
 

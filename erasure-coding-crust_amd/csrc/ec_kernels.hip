@@ -180,6 +180,69 @@ __global__ void __launch_bounds__(kBlock) error_locator_g(const uint8_t *__restr
   }
 }
 
+// The same folded locator with one WAVE per erasure pattern, for 64 <= n <= 4096
+// (round 3): V = n / 64 positions per lane (position lane * V + r), the Walsh
+// stages over register bits in registers and over the six lane bits by
+// __shfl_xor; no LDS, no barrier, four patterns per 256-thread workgroup.  The
+// workgroup form above spends ~20 barriers per pattern; at 4096 distinct
+// patterns (n = 1024) it took 43 us, this form ~5 us, which also makes the
+// pattern dedup (~35 us of hash / insert / resolve / broadcast kernels) cost
+// more than it can save for n <= 4096: ECCR_AMD_error_locator computes every
+// row directly there.  Results are congruent mod 65535 to the reference's
+// (the workgroup form's arithmetic, term for term).
+__device__ __forceinline__ uint32_t fold16(uint32_t s) { return (s & 0xffffu) + (s >> 16); }
+
+template <int V>
+__device__ __forceinline__ void walsh_wave(uint32_t (&w)[V], uint32_t lane) {
+#pragma unroll
+  for (int h = 1; h < V; h <<= 1)  // register bits
+#pragma unroll
+    for (int r = 0; r < V; ++r)
+      if (!(r & h)) {
+        const uint32_t x = w[r], y = w[r + h];
+        w[r] = fold16(x + y);
+        w[r + h] = fold16(x + 65535u - y);
+      }
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {  // lane bits: the partner is lane ^ 2^m
+    const bool upper = (lane >> m) & 1;
+#pragma unroll
+    for (int r = 0; r < V; ++r) {
+      const uint32_t o = uint32_t(__shfl_xor(int(w[r]), 1 << m));
+      w[r] = upper ? fold16(o + 65535u - w[r]) : fold16(w[r] + o);
+    }
+  }
+}
+
+template <int V>
+__global__ void __launch_bounds__(256) error_locator_w(const uint8_t *__restrict__ present, int nv,
+                                                       uint32_t rows,
+                                                       const uint16_t *__restrict__ fold,
+                                                       const uint32_t *__restrict__ pattern,
+                                                       uint16_t *__restrict__ elog) {
+  constexpr uint32_t n = 64 * V;
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= rows) return;                             // whole waves
+  if (pattern && pattern[b] != b) return;            // computed by its pattern's leader
+  const uint8_t *pr = present + uint64_t(b) * n + lane * V;
+  const uint16_t *F = fold + lane * V;
+  uint32_t w[V];
+  uint64_t erased = 0;
+#pragma unroll
+  for (int r = 0; r < V; ++r) {
+    const bool e = !(int(lane * V + r) < nv && pr[r]);
+    erased |= uint64_t(e) << r;
+    w[r] = e;
+  }
+  walsh_wave<V>(w, lane);
+#pragma unroll
+  for (int r = 0; r < V; ++r) w[r] = fold16(fold16(w[r] * uint32_t(F[r])));  // W * F mod 65535
+  walsh_wave<V>(w, lane);
+  uint16_t *E = elog + uint64_t(b) * n + lane * V;
+#pragma unroll
+  for (int r = 0; r < V; ++r) E[r] = uint16_t(((erased >> r) & 1) ? 65535u - w[r] : w[r]);
+}
+
 // ---- erasure-pattern dedup: payloads whose erasure
 // patterns are equal share one locator.  The locator depends only on the
 // flags (present[i] != 0) of positions i < nv, and so do the hash and the
@@ -394,6 +457,8 @@ int groups_for(uint32_t size) {  // byte-planar groups per workgroup
 
 }  // namespace
 
+bool locator_wave_applicable(uint32_t n) { return n >= 64 && n <= 4096; }
+
 size_t encode_scratch_bytes(const CodeParams &p, size_t plen, size_t batch) {
   if (k1024_applicable(p)) return k1024_scratch_bytes(plen, batch);
   if (p.k <= uint32_t(kLdsSlots)) return 0;
@@ -409,7 +474,11 @@ hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t 
   const bool aligned = (reinterpret_cast<uintptr_t>(d_payloads) % 16 == 0) &&
                        (reinterpret_cast<uintptr_t>(d_shards) % 8 == 0) &&
                        (batch == 1 || pstride % 16 == 0) && sstride % 8 == 0;
-  if (aligned && k256_applicable(p))
+  if (k256_applicable(p) &&
+      (k256_packed(plen, pstride, batch, reinterpret_cast<uintptr_t>(d_payloads),
+                   reinterpret_cast<uintptr_t>(d_shards), sstride)
+           ? k256_packed_ok(plen, batch, reinterpret_cast<uintptr_t>(d_shards), sstride)
+           : aligned))
     return launch_encode_k256(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
   if (aligned && encgen_applicable(p))
     return launch_encode_gen(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
@@ -464,6 +533,21 @@ hipError_t launch_error_locator(const CodeParams &p, const uint8_t *d_present, s
                                 const uint16_t *d_fold, const uint32_t *d_pattern,
                                 uint16_t *d_err_log, hipStream_t s) {
   if (batch == 0) return hipSuccess;
+  if (locator_wave_applicable(p.n)) {
+    const dim3 grid(unsigned((batch + 3) / 4));
+#define ECAMD_LOC_W(VV)                                                                          \
+  case VV:                                                                                       \
+    hipLaunchKernelGGL(error_locator_w<VV>, grid, dim3(256), 0, s, d_present, int(p.nv),         \
+                       uint32_t(batch), d_fold, d_pattern, d_err_log);                           \
+    break;
+    switch (p.n / 64) {
+      ECAMD_LOC_W(1) ECAMD_LOC_W(2) ECAMD_LOC_W(4) ECAMD_LOC_W(8) ECAMD_LOC_W(16) ECAMD_LOC_W(32)
+      ECAMD_LOC_W(64)
+      default: return hipErrorInvalidValue;
+    }
+#undef ECAMD_LOC_W
+    return hipGetLastError();
+  }
   const size_t shm = size_t(p.n) * sizeof(uint16_t);
   int cus = 0;
   if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&error_locator_g), 65536 * 2, &cus);
@@ -499,7 +583,11 @@ hipError_t launch_reconstruct(const CodeParams &p, const DevTables &t, const uin
   const bool aligned = (reinterpret_cast<uintptr_t>(d_shards) % 16 == 0) &&
                        (reinterpret_cast<uintptr_t>(d_out) % 8 == 0) && sstride % 16 == 0 &&
                        (batch == 1 || ostride % 8 == 0);
-  if (aligned && n1024_applicable(p))
+  const bool out8 = reinterpret_cast<uintptr_t>(d_out) % 8 == 0 && (batch == 1 || ostride % 8 == 0);
+  if (n1024_applicable(p) &&
+      (n1024_packed(slen, reinterpret_cast<uintptr_t>(d_shards), sstride)
+           ? out8 && reinterpret_cast<uintptr_t>(d_shards) % 2 == 0 && sstride % 2 == 0
+           : aligned))
     return launch_reconstruct_n1024(p, t, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch,
                                     d_out, ostride, scratch, s);
   if (aligned && n4096_applicable(p) && reinterpret_cast<uintptr_t>(d_out) % 16 == 0 &&

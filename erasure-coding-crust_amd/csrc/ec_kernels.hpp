@@ -47,6 +47,9 @@ hipError_t launch_error_locator(const CodeParams &p, const uint8_t *d_present, s
                                 uint16_t *d_err_log, hipStream_t s);
 // Pattern dedup: d_pattern[b] = the smallest index whose
 // erasure pattern equals payload b's.  Needs dedup_scratch_bytes(batch).
+// true if launch_error_locator runs the wave-per-pattern form (64 <= n <= 4096),
+// cheap enough that a batch computes every row instead of deduplicating
+bool locator_wave_applicable(uint32_t n);
 size_t dedup_scratch_bytes(size_t batch);
 hipError_t launch_dedup_patterns(const CodeParams &p, const uint8_t *d_present, size_t batch,
                                  uint32_t *d_pattern, void *scratch, hipStream_t s);
@@ -67,6 +70,12 @@ hipError_t launch_systematic(const CodeParams &p, const uint8_t *d_shards, size_
 
 // specialised kernels (enc_k256.hip)
 bool k256_applicable(const CodeParams &p);
+// reconstruct_n1024 runs packed (flattened columns, any even shard pitch)
+bool n1024_packed(size_t slen, uintptr_t sh, size_t sstride);
+// the packed (flattened-piece, any-alignment) encode_k256 applies: small
+// payloads or pitches the unpacked kernel cannot take; ..._ok: its own limits
+bool k256_packed(size_t plen, size_t pstride, size_t batch, uintptr_t pay, uintptr_t sh, size_t sstride);
+bool k256_packed_ok(size_t plen, size_t batch, uintptr_t sh, size_t sstride);
 hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                               size_t sstride, hipStream_t s);

@@ -271,14 +271,53 @@ __device__ __forceinline__ void stage_own(const State &s, uint8_t *xch, uint32_t
         to_be(s.l[0][r], s.h[0][r]);
 }
 
+// one 16-B chunk (8 pieces) of a shard row at any even address: the widest
+// stores the address allows, 2-B stores for a partial chunk (packed batches
+// with tight, unaligned row pitches)
+__device__ __forceinline__ void store_chunk_any(uint8_t *dst, const uint4 val, uint64_t nvalid) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(dst);
+  if (nvalid >= 8) {
+    if ((a & 15) == 0) {
+      *reinterpret_cast<uint4 *>(dst) = val;
+      return;
+    }
+    if ((a & 7) == 0) {
+      reinterpret_cast<uint2 *>(dst)[0] = make_uint2(val.x, val.y);
+      reinterpret_cast<uint2 *>(dst)[1] = make_uint2(val.z, val.w);
+      return;
+    }
+    if ((a & 3) == 0) {
+      reinterpret_cast<uint32_t *>(dst)[0] = val.x;
+      reinterpret_cast<uint32_t *>(dst)[1] = val.y;
+      reinterpret_cast<uint32_t *>(dst)[2] = val.z;
+      reinterpret_cast<uint32_t *>(dst)[3] = val.w;
+      return;
+    }
+  }
+  const uint32_t w[4] = {val.x, val.y, val.z, val.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    if (uint64_t(e) < nvalid) *reinterpret_cast<uint16_t *>(dst + 2 * e) = uint16_t(w[e >> 1] >> (16 * (e & 1)));
+}
+
 // all waves: rows [s0, s0 + 256) from the 16 regions -> shards; lane =
-// (row-in-4, source wave c = 16-B chunk of pieces [8c, 8c + 8)).
+// (row-in-4, source wave c = 16-B chunk of pieces [8c, 8c + 8)): pieces
+// piece0 + 8c of the tile's payload (SH), or, packed, pieces [pc, pc + 8) of
+// the payload bc that owns flattened slot tile * TILE + 8c (computed here, not
+// kept live across the FFTs)
+template <bool PACKED>
 __device__ __forceinline__ void store_own(const uint8_t *xbase, uint8_t *SH, uint64_t sstride,
-                                          uint32_t s0, int nv, uint64_t piece0,
-                                          uint64_t npieces, uint32_t wave, uint32_t lane) {
+                                          uint32_t s0, int nv, uint64_t piece0, uint64_t npieces,
+                                          uint32_t wave, uint32_t lane, uint64_t tile, uint32_t npp8,
+                                          uint32_t batch) {
   asm volatile("" : "+v"(lane));  // recomputed here, not kept live across the FFTs
   const uint32_t c = lane & 15;
-  const uint64_t p = piece0 + 8 * c;
+  uint64_t p = piece0 + 8 * c;
+  if constexpr (PACKED) {
+    const uint32_t gc = uint32_t(tile) * TILE + 8 * c, bc = gc / npp8;
+    p = bc < batch ? gc % npp8 : npieces;  // past the batch: nothing to store
+    SH += uint64_t(bc < batch ? bc : 0) * uint64_t(nv) * sstride;
+  }
   const bool wide = ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0;  // 16-B aligned rows
   const uint8_t *src = xbase + c * XCH_BYTES;
 #pragma unroll
@@ -288,7 +327,9 @@ __device__ __forceinline__ void store_own(const uint8_t *xbase, uint8_t *SH, uin
     const uint32_t shard = s0 + v;
     if (int(shard) >= nv) continue;
     uint8_t *dst = SH + uint64_t(shard) * sstride + 2 * p;
-    if (p + 8 <= npieces) {
+    if constexpr (PACKED) {
+      if (p < npieces) store_chunk_any(dst, val, npieces - p);
+    } else if (p + 8 <= npieces) {
       if (wide) {
         *reinterpret_cast<uint4 *>(dst) = val;
       } else {
@@ -303,17 +344,45 @@ __device__ __forceinline__ void store_own(const uint8_t *xbase, uint8_t *SH, uin
   }
 }
 
+// 16 payload bytes at any address, zero past `avail` (bytes valid from p):
+// aligned dwords that each hold at least one wanted byte (so nothing outside
+// the payload's allocation is touched), funnel-shifted by v_alignbyte
+__device__ __forceinline__ uint4 load16_any(const uint8_t *p, uint64_t avail) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  if (avail >= 16 && (a & 15) == 0) return *reinterpret_cast<const uint4 *>(p);
+  if (avail == 0) return make_uint4(0, 0, 0, 0);
+  const uint32_t sh = uint32_t(a & 3), nb = avail < 16 ? uint32_t(avail) : 16u;
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+  uint32_t d[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) d[i] = uint32_t(4 * i) < sh + nb ? q[i] : 0u;
+  uint32_t w[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+    const uint32_t have = nb > uint32_t(4 * j) ? nb - uint32_t(4 * j) : 0u;  // valid bytes of word j
+    if (have < 4) w[j] &= (1u << (8 * have)) - 1u;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 }  // namespace
 
 // N = n: 1024 (n_validators 766..1024) or 2048 (1025..1533); the cosets at
 // 1024 and above use LDS table image 1 (skews 1024 .. 2046, DevTables::timg)
 // at offset sh - 1024, reloaded by LDS-DMA between the two coset loops
-template <int N>
+// PACKED (small payloads, or payload / shard pitches the 16-B path cannot
+// take): tiles run over the flattened piece space of the batch, payload b
+// owning slots [b * npp8, b * npp8 + npieces) with npp8 = pieces rounded up
+// to 8, so a wave's 8 pieces (and each 16-B chunk of a staged row) belong to
+// one payload; loads and stores take any alignment.  4096 one-piece payloads
+// are 256 tiles instead of 4096.
+template <int N, bool PACKED>
 __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict__ payloads,
                                                        uint64_t plen, uint64_t pstride,
                                                        uint8_t *__restrict__ shards, uint64_t slen,
                                                        uint64_t sstride, int nv, uint32_t batch,
-                                                       DevTables t) {
+                                                       uint32_t npp8, DevTables t) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
   const uint32_t tid0 = threadIdx.x;
@@ -332,7 +401,7 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
 
   const uint64_t npieces = slen / 2;
   const uint32_t tiles_pp = uint32_t((npieces + TILE - 1) / TILE);
-  const uint64_t total = uint64_t(tiles_pp) * batch;
+  const uint64_t total = PACKED ? (uint64_t(npp8) * batch + TILE - 1) / TILE : uint64_t(tiles_pp) * batch;
   for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
     // lane ids made opaque per tile: per-lane LDS addresses are recomputed in the
     // loop instead of being hoisted out of it and spilled
@@ -345,10 +414,22 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     xb.a = mswz(ulaneA(q, inst));
     xb.b = mswz(ulaneB(q, inst));
     xb.c = mswz(ulaneC(q, inst));
-    const uint64_t b = tile / tiles_pp;
-    const uint64_t piece0 = (tile % tiles_pp) * TILE;
+    // unpacked: the tile is pieces [piece0, piece0 + 128) of payload b;
+    // packed: wave w's 8 pieces are pieces [pw, pw + 8) of payload bw (uniform),
+    // and the chunk a lane stores (source wave c) is pieces [pc, pc + 8) of bc
+    uint64_t b, piece0, bw = 0, pw = 0;
+    if constexpr (PACKED) {
+      const uint32_t gw = uint32_t(tile) * TILE + 8 * wave;  // < 2^32 (launch check)
+      bw = gw / npp8;
+      pw = gw % npp8;
+      b = bw;
+      piece0 = pw;
+    } else {
+      b = tile / tiles_pp;
+      piece0 = (tile % tiles_pp) * TILE;
+    }
     const uint8_t *P = payloads + b * pstride;
-    uint8_t *SH = shards + b * uint64_t(nv) * sstride;
+    uint8_t *SH = PACKED ? shards : shards + b * uint64_t(nv) * sstride;  // packed: per chunk
 
     // ---- load 8 pieces x 16 bytes (positions 8q..8q+7), zero past plen
     State s;
@@ -357,15 +438,22 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
       uint4 d[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const uint64_t piece = piece0 + wave * 8 * GP + inst * 4 * GP + g * 4 + u;
-        const uint64_t off = piece * 2 * K + 16 * q;
-        if (off + 16 <= plen) {
-          d[u] = *reinterpret_cast<const uint4 *>(P + off);
+        if constexpr (PACKED) {
+          const uint64_t piece = pw + inst * 4 * GP + g * 4 + u;
+          const uint64_t off = piece * 2 * K + 16 * q;
+          const bool ok = bw < batch && piece < npieces && off < plen;
+          d[u] = load16_any(P + (ok ? off : 0), ok ? plen - off : 0);
         } else {
-          uint32_t w[4] = {0, 0, 0, 0};
-          for (uint64_t e = off; e < plen && e < off + 16; ++e)
-            w[(e - off) >> 2] |= uint32_t(P[e]) << (8 * ((e - off) & 3));
-          d[u] = make_uint4(w[0], w[1], w[2], w[3]);
+          const uint64_t piece = piece0 + wave * 8 * GP + inst * 4 * GP + g * 4 + u;
+          const uint64_t off = piece * 2 * K + 16 * q;
+          if (off + 16 <= plen) {
+            d[u] = *reinterpret_cast<const uint4 *>(P + off);
+          } else {
+            uint32_t w[4] = {0, 0, 0, 0};
+            for (uint64_t e = off; e < plen && e < off + 16; ++e)
+              w[(e - off) >> 2] |= uint32_t(P[e]) << (8 * ((e - off) & 3));
+            d[u] = make_uint4(w[0], w[1], w[2], w[3]);
+          }
         }
       }
       // 4x4 byte transposes: dword j of each piece = (hi_{2j}, lo_{2j}, hi_{2j+1}, lo_{2j+1})
@@ -385,7 +473,7 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     lds_barrier();  // the other waves are done reading this region (last tile)
     stage_own(s, xch, q, inst, wave);
     lds_barrier();
-    store_own(stg, SH, sstride, 0, nv, piece0, npieces, wave, lane);
+    store_own<PACKED>(stg, SH, sstride, 0, nv, piece0, npieces, wave, lane, tile, npp8, batch);
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- IFFT_256 (index 0): passes A (bits 0-2), B (3-5), C (6-7)
@@ -420,7 +508,7 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
       fpass3(s, tabs, posA(q, 0), 0, off);
       stage_own(s, xch, q, inst, wave);
       lds_barrier();
-      store_own(stg, SH, sstride, sh, nv, piece0, npieces, wave, lane);
+      store_own<PACKED>(stg, SH, sstride, sh, nv, piece0, npieces, wave, lane, tile, npp8, batch);
       __builtin_amdgcn_sched_barrier(0);
     };
     if constexpr (N == 1024) {
@@ -439,24 +527,49 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
 
 bool k256_applicable(const CodeParams &p) { return p.k == 256 && (p.n == 1024 || p.n == 2048); }
 
+// packed tiles: pieces per payload below one tile, or pitches / bases the
+// unpacked kernel's 16-B loads and 8-B stores cannot take (any even shard
+// pitch and shard base, any payload pitch and base)
+bool k256_packed(size_t plen, size_t pstride, size_t batch, uintptr_t pay, uintptr_t sh, size_t sstride) {
+  const size_t npp = (plen + 2 * K - 1) / (2 * K);
+  const bool aligned = pay % 16 == 0 && sh % 8 == 0 && (batch == 1 || pstride % 16 == 0) && sstride % 8 == 0;
+  return !aligned || npp < size_t(TILE);
+}
+
+bool k256_packed_ok(size_t plen, size_t batch, uintptr_t sh, size_t sstride) {
+  const size_t npp8 = ((plen + 2 * K - 1) / (2 * K) + 7) / 8 * 8;
+  return sh % 2 == 0 && sstride % 2 == 0 && npp8 * batch + TILE < (size_t(1) << 32);
+}
+
 hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                               size_t sstride, hipStream_t s) {
   int cus = 0;
-  const void *fn = p.n == 1024 ? reinterpret_cast<const void *>(&encode_k256<1024>)
-                               : reinterpret_cast<const void *>(&encode_k256<2048>);
+  const bool packed = k256_packed(plen, pstride, batch, reinterpret_cast<uintptr_t>(d_payloads),
+                                  reinterpret_cast<uintptr_t>(d_shards), sstride);
+  if (packed && !k256_packed_ok(plen, batch, reinterpret_cast<uintptr_t>(d_shards), sstride))
+    return hipErrorInvalidValue;
+  const void *fn = p.n == 1024 ? (packed ? reinterpret_cast<const void *>(&encode_k256<1024, true>)
+                                         : reinterpret_cast<const void *>(&encode_k256<1024, false>))
+                               : (packed ? reinterpret_cast<const void *>(&encode_k256<2048, true>)
+                                         : reinterpret_cast<const void *>(&encode_k256<2048, false>));
   if (const hipError_t e = prepare_kernel(fn, LDS_BYTES, &cus); e != hipSuccess) return e;
   const size_t sl = shard_len(p.k, plen);
-  const size_t tiles = (sl / 2 + TILE - 1) / TILE * batch;
+  const size_t npp8 = (sl / 2 + 7) / 8 * 8;
+  const size_t tiles = packed ? (npp8 * batch + TILE - 1) / TILE : (sl / 2 + TILE - 1) / TILE * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
-  if (p.n == 1024)
-    hipLaunchKernelGGL(encode_k256<1024>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
-                       uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl),
-                       uint64_t(sstride), int(p.nv), uint32_t(batch), t);
-  else
-    hipLaunchKernelGGL(encode_k256<2048>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
-                       uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl),
-                       uint64_t(sstride), int(p.nv), uint32_t(batch), t);
+#define ECAMD_K256(NN, PK)                                                                       \
+  hipLaunchKernelGGL((encode_k256<NN, PK>), dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,   \
+                     uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride), \
+                     int(p.nv), uint32_t(batch), uint32_t(npp8), t)
+  if (p.n == 1024) {
+    if (packed) ECAMD_K256(1024, true);
+    else ECAMD_K256(1024, false);
+  } else {
+    if (packed) ECAMD_K256(2048, true);
+    else ECAMD_K256(2048, false);
+  }
+#undef ECAMD_K256
   return hipGetLastError();
 }
 

@@ -743,7 +743,8 @@ def test_graph_capture_ws(oracle, nv, plen, batch, use_ws):
     sl = E.shard_len(nv, plen)
     ss = (sl + 63) // 64 * 64
     need = E.workspace_bytes(nv, plen, batch)
-    assert need[1] > 0 and (nv > 4096 or need[2] > 0)  # the shapes do need scratch
+    # the shapes do need scratch; the locator only where it deduplicates (n > 4096)
+    assert (need[1] > 0) == (n > 4096) and (nv > 4096 or need[2] > 0)
     ws = torch.empty(max(need), dtype=torch.uint8, device="cuda")
     d_pay = torch.empty((batch, plen), dtype=torch.uint8, device="cuda")
     d_sh = torch.full((batch, nv, ss), 0xAA, dtype=torch.uint8, device="cuda")
@@ -812,7 +813,9 @@ def test_workspace_too_small_is_reported():
     assert e.value.tag == E.Tag.UNKNOWN_RECONSTRUCTION and "workspace" in E.last_error()
     big = torch.empty(max(wl, wr) + 512, dtype=torch.uint8, device="cuda")
     with pytest.raises(E.ECError):  # misaligned
-        E.error_locator_ws(nv, d_pr, batch, d_el, big[1:])
+        E.reconstruct_batch_ws(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k, big[1:])
+    assert wl == 0  # n <= 4096: the locator computes every row, no dedup scratch
+    E.error_locator_ws(nv, d_pr, batch, d_el, big[1:])  # needs none, so any workspace will do
     torch.cuda.synchronize()
     assert bool((d_out == 0x5A).all())
 
@@ -920,3 +923,87 @@ def test_fresh_process_concurrent_first_calls():
                               orc=os.path.join(root, "oracle"))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+
+
+# ------------------------------------------- packed small-payload kernels (round 3)
+@pytest.mark.parametrize("nv,plen,batch,layout", [
+    (1024, 1, 37, "tight"), (1024, 15, 300, "tight"), (1024, 15, 64, "pad64"), (1024, 300, 129, "tight"),
+    (1024, 511, 9, "odd"), (1024, 512, 33, "tight"), (1024, 513, 17, "pad16"), (1024, 3001, 21, "odd"),
+    (1024, 5000, 40, "tight"), (1024, 5000, 24, "pad64"), (1024, 16385, 5, "odd"), (1024, 65535, 3, "tight"),
+    (1024, 70001, 3, "odd"),                     # > 64 KB with odd pitches: packed tiles too
+    (800, 300, 45, "tight"), (1000, 20000, 7, "pad16"), (766, 15, 80, "odd"),
+    (1025, 300, 31, "tight"), (1500, 5000, 9, "odd")])  # n = 2048 encode (packed) / reconstruct_n4096
+def test_packed_small_batches(oracle, nv, plen, batch, layout):
+    """Small payloads (the benchmark/ sizes) and pitches the 16-B kernels cannot
+    take run the packed encode_k256 / reconstruct_n1024 (flattened pieces /
+    columns across payloads, any alignment): every shard byte and every output
+    byte vs the oracle, shard rows and outputs prefilled with 0xAA (a write
+    past a payload's pieces or columns shows up), absent rows overwritten with
+    garbage.  tight: pitch = length; odd: odd payload base and pitch, shard
+    pitch = shard_len + 2; padNN: pitches rounded to NN bytes."""
+    import torch
+    n, k, thr = E.code_params(nv)
+    sl = E.shard_len(nv, plen)
+    if layout == "tight":
+        ps, ss, off = plen, sl, 0
+    elif layout == "odd":
+        ps, ss, off = plen + 3, sl + 2, 1
+    else:
+        pad = int(layout[3:])
+        ps, ss, off = (plen + pad - 1) // pad * pad, (sl + pad - 1) // pad * pad, 0
+    rng = np.random.default_rng(nv * 31 + plen)
+    pay = np.stack([synth.payload(70_000 + 13 * b + plen, plen) for b in range(batch)])
+    buf = np.zeros(off + batch * ps + 8, dtype=np.uint8)
+    for b in range(batch):
+        buf[off + b * ps: off + b * ps + plen] = pay[b]
+    d_buf = torch.from_numpy(buf).cuda()
+    d_pay = d_buf[off:]
+    d_sh = _prefilled((batch * nv * ss,))
+    E.encode_batch(nv, d_pay, plen, ps, batch, d_sh, ss)
+    torch.cuda.synchronize()
+    shv = d_sh.cpu().numpy().reshape(batch, nv, ss)
+    refs = []
+    for b in range(batch):
+        ref = oracle.encode(nv, pay[b].tobytes())
+        refs.append(ref)
+        assert [shv[b, v, :sl].tobytes() for v in range(nv)] == ref, (b, "encode")
+        assert (shv[b, :, sl:] == 0xAA).all(), (b, "shard pitch bytes written")
+    cnts = [k, thr, nv]
+    pres = np.stack([synth.present_mask(90_000 + b, nv, cnts[b % 3], n) for b in range(batch)])
+    d_pr = torch.from_numpy(pres).cuda()
+    for b in range(batch):  # absent rows: garbage that must never be read
+        gone = np.where(pres[b][:nv] == 0)[0]
+        if len(gone):
+            d_sh.view(batch, nv, ss)[b, torch.from_numpy(gone).cuda()] = 0x5C
+    d_el = torch.zeros((batch, n), dtype=torch.int16, device="cuda")
+    d_out = _prefilled((batch, sl * k))
+    E.error_locator(nv, d_pr, batch, d_el)
+    E.reconstruct_batch(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    for b in range(batch):
+        keep = [refs[b][i] if pres[b][i] else None for i in range(nv)]
+        assert out[b].tobytes() == oracle.reconstruct(nv, keep), (b, "reconstruct")
+        assert out[b, :plen].tobytes() == pay[b].tobytes()
+
+
+def test_locator_rows_every_pattern(oracle):
+    """The wave-per-pattern error locator (64 <= n <= 4096) on a batch of
+    distinct and repeated patterns, every row mod 65535 vs oracle.error_poly,
+    for each n it covers; rows past the batch untouched."""
+    import torch
+    for nv in (33, 64, 100, 200, 300, 600, 1000, 1024, 1500, 2048, 3000, 4096):
+        n, k, thr = E.code_params(nv)
+        batch = 11
+        pres = np.stack([synth.present_mask(5_000 + nv + (b % 7), nv, [k, thr, nv][b % 3], n)
+                         for b in range(batch)])
+        d_pr = torch.from_numpy(pres).cuda()
+        d_el = torch.full((batch + 1, n), 0x1234, dtype=torch.int16, device="cuda")
+        E.error_locator(nv, d_pr, batch, d_el)
+        torch.cuda.synchronize()
+        el = d_el.cpu().numpy().view(np.uint16)
+        assert (el[batch] == 0x1234).all(), nv
+        for b in range(batch):
+            erased = (pres[b][:n] == 0).astype(np.uint8)
+            ep = oracle.error_poly(erased, n)[:n].astype(np.int64) % 65535
+            assert ((el[b].astype(np.int64) % 65535) == ep).all(), (nv, b)
