@@ -143,6 +143,112 @@ def cpu_baseline(nv, plen, cnt, seconds):
     return res
 
 
+# the reference's own benchmark sizes (benchmark/benchmark.cpp:36-45,
+# README.md:50-84) and the per-GPU batch each is measured on
+BENCH_SIZES = (15, 300, 5000, 100_000, 1_000_000, 10_000_000)
+SWEEP_BATCH = {15: 4096, 300: 4096, 5000: 4096, 100_000: 1024, 1_000_000: 4096, 10_000_000: 400}
+
+
+def cpu_size_rate(nv, plen, cnt, seconds, threads):
+    """ec-cpp (oracle/_ref) encode + reconstruct rate at one payload size on
+    this host: 1 thread and `threads` threads (one payload per thread)."""
+    import oracle as orc
+    if not orc.RefEC.available():
+        return None
+    ref = orc.RefEC()
+    p = synth.payload(424242 + plen, plen).tobytes()
+    present = synth.present_mask(10**6 + plen, nv, cnt)
+    d1, w1, _, _ = ref.time_mt(nv, p, present, 1, seconds)
+    dn, wn, _, _ = ref.time_mt(nv, p, present, threads, seconds)
+    return {"GiBps_1thread": round(d1 * plen / w1 / 2**30, 6),
+            f"GiBps_{threads}threads": round(dn * plen / wn / 2**30, 6)}
+
+
+def size_sweep(args, nv, cnt_key, dev, stream, dist, world, rank, backend, headline):
+    """Device-resident encode + locator + reconstruct at each benchmark/ size
+    (north_star): the same step as the headline on synthetic payloads of that
+    size, tight payload pitch (the packed kernels take small payloads), shard
+    rows padded to 64 B; per size the whole-job GiB/s (max-over-ranks time),
+    the dominant kernel's HBM roofline fraction, and ec-cpp on this host's
+    cores beside it (rank 0).  Shard rows shorter than 64 B are tight (the
+    reference's own shard buffers are exactly shard_len long).  The 1 MB row is
+    the headline measurement."""
+    n, k, thr = E.code_params(nv)
+    cnt = {"threshold": thr, "k": k}.get(cnt_key) or int(cnt_key)
+    threads = max(1, min(len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 1, 16))
+    rows = []
+    for plen in args.sweep_sizes:
+        if plen == args.payload and args.batch == SWEEP_BATCH.get(plen) and headline is not None:
+            row = dict(headline)
+        else:
+            B = SWEEP_BATCH.get(plen, max(1, min(4096, (4 << 30) // max(plen, 1))))
+            sl = E.shard_len(nv, plen)
+            # shard rows padded to 64 B (aligned vector stores), except rows
+            # shorter than that, which stay tight: a 2-byte shard in a 64-byte
+            # slot would make every shard write its own HBM burst (32x the bytes)
+            ss = (sl + 63) // 64 * 64 if sl >= 64 else sl
+            seeds = sharding.rank_seeds(rank, B)
+            d_pay = torch.empty((B, plen), dtype=torch.uint8, device=dev)
+            for c0 in range(0, B, 256):
+                d_pay[c0:c0 + 256] = synth.payloads_torch(seeds[c0:c0 + 256], plen, device=dev)
+            d_pres = torch.from_numpy(synth.present_masks([10**6 + s for s in seeds], nv, cnt, n)).to(dev)
+            d_sh = torch.empty((B, nv, ss), dtype=torch.uint8, device=dev)
+            d_el = torch.empty((B, n), dtype=torch.int16, device=dev)
+            d_out = torch.empty((B, sl * k), dtype=torch.uint8, device=dev)
+            ev = []
+
+            def step(record):
+                if record:
+                    e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                    e[0].record(stream)
+                E.encode_batch(nv, d_pay, plen, plen, B, d_sh, ss, stream)
+                if record:
+                    e[1].record(stream)
+                E.error_locator(nv, d_pres, B, d_el, stream)
+                if record:
+                    e[2].record(stream)
+                E.reconstruct_batch(nv, d_sh, sl, ss, d_pres, d_el, B, d_out, sl * k, stream)
+                if record:
+                    e[3].record(stream)
+                    ev.append(e)
+
+            for _ in range(args.warmup):
+                step(False)
+            torch.cuda.synchronize(dev)
+            if dist:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step(True)
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            if dist:
+                dist.barrier()
+            el = sharding.max_over_ranks(t1 - t0, dist, dev if backend == "nccl" else None)
+            ok = bool(torch.equal(d_out[:, :plen], d_pay))
+            ms = lambda a, b: float(np.mean([x[a].elapsed_time(x[b]) for x in ev]))  # noqa: E731
+            t_enc, t_loc, t_rec = ms(0, 1), ms(1, 2), ms(2, 3)
+            kern = {"encode": (t_enc, B * (plen + nv * sl)),
+                    "reconstruct": (t_rec, B * (cnt + k) * sl + B * n * 2)}
+            dom = max(kern, key=lambda x: kern[x][0])
+            achieved = kern[dom][1] / (kern[dom][0] * 1e-3)
+            row = {"payload_bytes": plen, "batch_per_gpu": B,
+                   "ms_per_step": round(el / args.steps * 1e3, 4),
+                   "GiBps": round(world * B * plen * args.steps / el / 2**30, 3),
+                   "kernels_ms": {"encode": round(t_enc, 4), "error_locator": round(t_loc, 4),
+                                  "reconstruct": round(t_rec, 4)},
+                   "roofline": {"kernel": dom, "achieved_GBps": round(achieved / 1e9, 2),
+                                "frac": round(achieved / HBM_PEAK, 5)},
+                   "roundtrip_ok": ok}
+            del d_pay, d_pres, d_sh, d_el, d_out
+            torch.cuda.empty_cache()
+        if rank == 0 and not args.no_cpu_baseline:
+            row["cpu_ec_cpp"] = cpu_size_rate(nv, plen, cnt, args.sweep_cpu_seconds, threads)
+        rows.append(row)
+    return rows
+
+
 def scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out, step_s, timeout_s,
                    on_timeout=None):
     """SURVEY.md §8e / north_star: the batch starts on GPU0 and the decoded
@@ -233,10 +339,17 @@ def main():
     ap.add_argument("--no-scatter", action="store_true",
                     help="skip the RCCL scatter / gather phase (N > 1)")
     ap.add_argument("--scatter-timeout", type=float, default=180.0)
+    ap.add_argument("--sweep", default="bench",
+                    help="'bench': also measure the benchmark/ payload sizes (15 B .. 10 MB) at "
+                         "n_validators=nv and report them in `sizes`; 'none': skip; or a comma list")
+    ap.add_argument("--sweep-cpu-seconds", type=float, default=0.5,
+                    help="ec-cpp sample per size and thread count in the sweep")
     ap.add_argument("--graph", action="store_true",
                     help="time K replays of one captured hipGraph step (ECCR_AMD_*_ws calls on "
                          "caller-owned scratch) instead of K eager steps")
     args = ap.parse_args()
+    args.sweep_sizes = (() if args.sweep == "none" else BENCH_SIZES if args.sweep == "bench"
+                        else tuple(int(x) for x in args.sweep.split(",")))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -374,6 +487,15 @@ def main():
     }
     if graph is not None:
         line["graph"] = "timed steps are hipGraph replays of one captured step; kernels_ms from eager steps"
+    if args.sweep_sizes:
+        headline = {"payload_bytes": plen, "batch_per_gpu": B, "ms_per_step": line["ms_per_step"],
+                    "GiBps": line["value"], "kernels_ms": line["kernels_ms"],
+                    "roofline": {"kernel": dom, "achieved_GBps": line["roofline"]["achieved"],
+                                 "frac": line["roofline"]["frac"]},
+                    "roundtrip_ok": ok, "note": "the headline measurement above"}
+        line["sizes"] = size_sweep(args, nv, args.present, dev, stream, dist, world, rank, backend,
+                                   headline)
+        ok = ok and all(r["roundtrip_ok"] for r in line["sizes"])
     if backend != "nccl":
         line["rehearsal"] = f"{world} ranks on {line['n_gpus']} GPU(s), gloo"
     if rank == 0 and not args.no_cpu_baseline:

@@ -178,25 +178,20 @@ __device__ __forceinline__ void swap_bit(uint32_t &x, uint32_t &y, int b, bool h
 
 __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ? 0u : c; }
 
-// 8 shard bytes at any even address, zero past `avail` (bytes valid from p):
-// aligned dwords that each hold at least one wanted byte, funnel-shifted
+// 8 shard bytes at any even address, zero past `avail` (1..8 bytes valid
+// from p): three dword loads, each clamped to the dword that holds the last
+// wanted byte (so nothing past the row is touched), funnel-shifted by
+// v_alignbyte; no branches
 __device__ __forceinline__ uint2 load8_any(const uint8_t *p, uint32_t avail) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  if (avail >= 8 && (a & 7) == 0) return *reinterpret_cast<const uint2 *>(p);
-  if (avail == 0) return make_uint2(0, 0);
-  const uint32_t sh = uint32_t(a & 3), nb = avail < 8 ? avail : 8u;
-  const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
-  uint32_t d[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) d[i] = uint32_t(4 * i) < sh + nb ? q[i] : 0u;
-  uint32_t w[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
-    const uint32_t have = nb > uint32_t(4 * j) ? nb - uint32_t(4 * j) : 0u;
-    if (have < 4) w[j] &= (1u << (8 * have)) - 1u;
-  }
-  return make_uint2(w[0], w[1]);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p), a0 = a & ~uintptr_t(3);
+  const uintptr_t last = (a + avail - 1) & ~uintptr_t(3);
+  const uint32_t sh = uint32_t(a & 3);
+  const uint32_t d0 = *reinterpret_cast<const uint32_t *>(a0);
+  const uint32_t d1 = *reinterpret_cast<const uint32_t *>(a0 + 4 < last ? a0 + 4 : last);
+  const uint32_t d2 = *reinterpret_cast<const uint32_t *>(a0 + 8 < last ? a0 + 8 : last);
+  const uint64_t keep = avail >= 8 ? ~0ull : (1ull << (8 * avail)) - 1;
+  return make_uint2(__builtin_amdgcn_alignbyte(d1, d0, sh) & uint32_t(keep),
+                    __builtin_amdgcn_alignbyte(d2, d1, sh) & uint32_t(keep >> 32));
 }
 
 // The two waves of a SIMD (w, w + 4) take turns at the higher issue priority
@@ -266,13 +261,14 @@ hipError_t launch_gather_order(const CodeParams &p, const uint8_t *d_present,
 size_t gather_order_bytes(const CodeParams &p, size_t batch) { return batch * p.n * sizeof(uint32_t); }
 
 // PACKED (payloads of fewer than 32 columns, or shard pitches the 16-B row
-// loads cannot take): tiles run over the flattened column space, payload b
-// owning columns [b * ncols4, b * ncols4 + ncols) with ncols4 = columns rounded
-// up to 4, so each byte-planar group (one wave's codewords) belongs to one
-// payload; the 8 groups of a tile may belong to 8 payloads.  The gather then
-// reads each (row, group) with that payload's flag and E[v] (natural row
-// order: no gather order), and the output goes to the wave's payload.  4096
-// one-column payloads are 512 tiles instead of 4096.
+// loads cannot take): the waves run independently over the flattened space
+// of byte-planar groups, payload b owning groups [b * ncols4 / 4, (b + 1) *
+// ncols4 / 4) (ncols4 = columns rounded up to 4), one group (4 codewords) per
+// wave and step.  Lane l gathers rows 16 l .. 16 l + 15 straight into the
+// IFFT's layout-A registers (its flags and E[v] in three coalesced loads, the
+// absent rows multiplied by the zero table), so there is no LDS gather, no
+// gather order and no workgroup barrier: 4096 one-column payloads are 4096
+// wave steps (2 per wave on 256 CUs) instead of 4096 workgroup tiles.
 template <bool PACKED>
 __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
@@ -295,7 +291,16 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
 
   const uint64_t ncols = slen / 2;
   const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);
-  const uint64_t total = PACKED ? (uint64_t(ncols4) * batch + COLS - 1) / COLS : uint64_t(tiles_pp) * batch;
+  const uint32_t gpp = ncols4 / 4;  // packed: groups per payload
+  // packed: "tile" = this wave's group, stepping over the grid's waves
+  const uint64_t total = PACKED ? uint64_t(gpp) * batch : uint64_t(tiles_pp) * batch;
+  // the wave index as a wave-uniform (scalar) value: the packed loop and every
+  // address derived from its group stay in SGPRs
+  const uint32_t wave_s = __builtin_amdgcn_readfirstlane(tid0 >> 6);
+  // (group g on workgroup g % grid, wave g / grid: a small batch spreads over
+  // every CU)
+  const uint64_t first = PACKED ? uint64_t(wave_s) * gridDim.x + blockIdx.x : blockIdx.x;
+  const uint64_t step = PACKED ? uint64_t(gridDim.x) * WAVES : gridDim.x;
   // m[0], m[1]: this thread's two gather slots (gather_order): row << 16 |
   // mul_index(E[row]), low half 0xFFFF = absent.  Loaded one tile ahead so the
   // gather's table loads wait on one global latency instead of two.
@@ -303,13 +308,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   // each: 0xFFFF = present (copied from the staged row), else mul_index(E[y]) (the
   // erased value is scaled by E[y]; y < 256 < nv always holds for n = 1024).
   auto load_meta = [&](uint64_t tl, uint32_t tid, uint32_t (&m)[4]) {
-    uint64_t bb;
-    if constexpr (PACKED) {  // the payload of this wave's group (phase 5 only)
-      bb = (uint32_t(tl) * COLS + 4 * (tid >> 6)) / ncols4;
-      if (bb >= batch) bb = 0;  // no output is written for it
-    } else {
-      bb = tl / tiles_pp;
-    }
+    const uint64_t bb = PACKED ? uint64_t(uint32_t(tl) / gpp) : tl / tiles_pp;
     const uint64_t pt = pattern ? pattern[bb] : bb;
     if constexpr (!PACKED) {
 #pragma unroll
@@ -327,8 +326,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     }
   };
   uint32_t meta[4] = {0, 0, 0, 0}, meta_next[4] = {0, 0, 0, 0};
-  if (blockIdx.x < total) load_meta(blockIdx.x, tid0, meta);
-  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+  if (first < total) load_meta(first, tid0, meta);
+  for (uint64_t tile = first; tile < total; tile += step) {
     // lane-derived addresses are recomputed per tile from an opaque copy of
     // the thread id (hoisted out of the loop they were kept live, and spilled,
     // across the whole tile)
@@ -336,43 +335,60 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63;
     uint64_t b, col0;
-    if constexpr (PACKED) {  // this wave's group: columns [col0, col0 + 4) of payload b
-      const uint32_t gw = uint32_t(tile) * COLS + 4 * (tid >> 6);
-      b = gw / ncols4;
-      col0 = uint64_t(gw % ncols4) - 4 * uint64_t(tid >> 6);  // cbase below = col0 + 4 * wave (mod 2^64)
+    if constexpr (PACKED) {  // this wave's group: columns [cbase, cbase + 4) of payload b
+      b = uint32_t(tile) / gpp;  // < 2^32 groups (launch check)
+      col0 = 4 * uint64_t(uint32_t(tile) % gpp) - 4 * uint64_t(wave_s);  // cbase below = col0 + 4 * wave (mod 2^64)
     } else {
       b = tile / tiles_pp;
       col0 = (tile % tiles_pp) * COLS;
     }
     const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
     uint8_t *O = out + b * ostride;
+    S16 s;
 
     if constexpr (PACKED) {
-      // ---- phase 1, packed: rows v = tid and tid + 512 (natural order), each
-      // with the 8 groups' own payloads: flag, E[v], 8 bytes (decode_main:174-177)
-      lds_barrier();  // previous tile's readers of the regions are done (LDS only)
+      // ---- phase 1, packed: rows v = 16 lane + r (layout A) of this wave's
+      // group, flags and E[v] of the payload's pattern (decode_main:174-177);
+      // absent rows (and rows >= nv) take the zero table and read no bytes
+      const uint64_t pt = pattern ? pattern[b] : b;
+      const uint32_t v0 = 16 * lane;
+      const uint4 f16 = *reinterpret_cast<const uint4 *>(present + pt * N + v0);
+      const uint4 e0 = *reinterpret_cast<const uint4 *>(elog + pt * N + v0);
+      const uint4 e1 = *reinterpret_cast<const uint4 *>(elog + pt * N + v0 + 8);
+      const uint32_t fw[4] = {f16.x, f16.y, f16.z, f16.w};
+      const uint32_t ew[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+      const uint64_t cg = 4 * uint64_t(uint32_t(tile) % gpp);
+      const uint64_t have = ncols - cg;  // columns of the group inside the payload
+      const uint32_t avail = have >= 4 ? 8u : uint32_t(2 * have);
+      const uint8_t *rowp = SH + uint64_t(v0) * sstride + 2 * cg;
+      // rows 8-B aligned and the group whole: one 8-B load per row (uniform)
+      const bool wide = avail == 8 && ((sstride | reinterpret_cast<uintptr_t>(rowp)) & 7) == 0;
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const uint32_t v = tid + half * THREADS;
+      for (int q = 0; q < 4; ++q) {  // 4 rows at a time: 4 tables + 4 rows in flight
+        Tab T[4];
+        uint2 d[4];
 #pragma unroll
-        for (int g = 0; g < 8; ++g) {
-          const uint32_t gg = uint32_t(tile) * COLS + 4 * g, bg = gg / ncols4, cg = gg % ncols4;
-          uint32_t l = 0, h = 0;
-          if (bg < batch && int(v) < nv) {
-            const uint64_t pt = pattern ? pattern[bg] : bg;
-            if (present[pt * N + v]) {
-              Tab T;
-              load_tab(t.mtab, mul_index(elog[pt * N + v]), T);
-              const uint64_t have = ncols - cg;  // columns of the group inside the payload
-              const uint2 d = load8_any(shards + uint64_t(bg) * nv * sstride + uint64_t(v) * sstride + 2 * cg,
-                                        have >= 4 ? 8u : uint32_t(2 * have));
-              if (v < uint32_t(K)) *reinterpret_cast<uint2 *>(stage + stage_addr(v, g)) = d;
-              const uint32_t xh = vperm(d.y, d.x, 0x06040200u), xl = vperm(d.y, d.x, 0x07050301u);
-              mul_acc(xl, xh, T, l, h);
-            }
-          }
-          *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l, h);
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * q + i;
+          const bool on = (fw[r >> 2] >> (8 * (r & 3))) & 0xFFu && int(v0) + r < nv;
+          const uint32_t e = (ew[r >> 1] >> (16 * (r & 1))) & 0xFFFFu;
+          load_tab(t.mtab, on ? mul_index(e) : 65535u, T[i]);  // mtab[65535] = * 0
+          d[i] = make_uint2(0, 0);
+          if (on) d[i] = wide ? *reinterpret_cast<const uint2 *>(rowp + uint64_t(r) * sstride)
+                              : load8_any(rowp + uint64_t(r) * sstride, avail);
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * q + i;
+          if (v0 + r < uint32_t(K)) *reinterpret_cast<uint2 *>(stage + stage_addr(v0 + r, wave)) = d[i];
+          const uint32_t xh = vperm(d[i].y, d[i].x, 0x06040200u), xl = vperm(d[i].y, d[i].x, 0x07050301u);
+          uint32_t l = 0, h = 0;
+          mul_acc(xl, xh, T[i], l, h);
+          // into the wave's own region (layout A, read back below): keeps the
+          // register live ranges those of the unpacked kernel
+          *reinterpret_cast<uint2 *>(my + raddr(v0 + r)) = make_uint2(l, h);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one batch of tables live at a time
       }
     } else {
     // ---- phase 1: gather + scale this thread's two slots' rows (present rows
@@ -433,9 +449,9 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l[g], h[g]);
     }
     }
-    if (tile + gridDim.x < total) load_meta(tile + gridDim.x, tid, meta_next);
+    if (tile + step < total) load_meta(tile + step, tid, meta_next);
     STAMP(2);
-    __syncthreads();
+    if constexpr (!PACKED) __syncthreads();  // packed: the wave's own region and staging only
     STAMP(3);
     // phase-5 tables requested now, consumed after the transform (latency
     // hidden behind it): E[y] of this lane's erased output rows y = 4 lane + q
@@ -445,13 +461,17 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t m = (meta[2 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
-      if (m != 0xFFFFu) load_tab(t.mtab, m, T5[q]);
+      if constexpr (PACKED) load_tab(t.mtab, m != 0xFFFFu ? m : 0u, T5[q]);  // defined on every path
+      else if (m != 0xFFFFu) load_tab(t.mtab, m, T5[q]);
     }
 
     // ---- phase 2: IFFT_1024 on this wave's group
-    S16 s;
     {  // layout A: v = 16*lane + r
       const uint32_t la = lds_addr(my) | raddr(16 * lane);
+      if constexpr (PACKED) {  // the wave's own writes above: a wave barrier orders them
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const uint2 x = lds_ld2(la ^ raddr(r));
@@ -683,7 +703,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const uint64_t col = cbase + c;
-        if (col >= ncols || (PACKED && b >= batch)) break;
+        if (col >= ncols) break;
         const uint32_t w0 = vperm(ol[0], oh[0], 0x0c0c0400u + 0x0101u * c) |
                             (vperm(ol[1], oh[1], 0x0c0c0400u + 0x0101u * c) << 16);
         const uint32_t w1 = vperm(ol[2], oh[2], 0x0c0c0400u + 0x0101u * c) |
@@ -732,7 +752,7 @@ hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
         e != hipSuccess)
       return e;
   }
-  const size_t tiles = packed ? (ncols4 * batch + COLS - 1) / COLS : (slen / 2 + COLS - 1) / COLS * batch;
+  const size_t tiles = packed ? ncols4 / 4 * batch : (slen / 2 + COLS - 1) / COLS * batch;  // packed: groups
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   if (packed)
     hipLaunchKernelGGL(reconstruct_n1024<true>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards,

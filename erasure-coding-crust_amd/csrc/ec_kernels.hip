@@ -583,11 +583,13 @@ hipError_t launch_reconstruct(const CodeParams &p, const DevTables &t, const uin
   const bool aligned = (reinterpret_cast<uintptr_t>(d_shards) % 16 == 0) &&
                        (reinterpret_cast<uintptr_t>(d_out) % 8 == 0) && sstride % 16 == 0 &&
                        (batch == 1 || ostride % 8 == 0);
-  const bool out8 = reinterpret_cast<uintptr_t>(d_out) % 8 == 0 && (batch == 1 || ostride % 8 == 0);
+  const bool out8 = reinterpret_cast<uintptr_t>(d_out) % 8 == 0 && (batch == 1 || ostride % 8 == 0) &&
+                    reinterpret_cast<uintptr_t>(d_present) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(d_err_log) % 16 == 0;  // vector loads of flag / E rows
   if (n1024_applicable(p) &&
       (n1024_packed(slen, reinterpret_cast<uintptr_t>(d_shards), sstride)
            ? out8 && reinterpret_cast<uintptr_t>(d_shards) % 2 == 0 && sstride % 2 == 0
-           : aligned))
+           : aligned && out8))
     return launch_reconstruct_n1024(p, t, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch,
                                     d_out, ostride, scratch, s);
   if (aligned && n4096_applicable(p) && reinterpret_cast<uintptr_t>(d_out) % 16 == 0 &&

@@ -366,18 +366,43 @@ __device__ __forceinline__ uint4 load16_any(const uint8_t *p, uint64_t avail) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// packed waves (PK = 2): this wave's 8 staged pieces x 256 rows [s0, s0 + 256)
+// -> shards, lane = (piece e = lane & 7, rows lane / 8 + 8 k); piece e of the
+// task is flattened piece 8 task + e, i.e. piece p of payload b (each piece
+// its own payload when payloads are one piece long): 2-B stores
+__device__ __forceinline__ void store_wave(const uint8_t *xch, uint8_t *shards, uint64_t sstride,
+                                           uint32_t s0, int nv, uint32_t task, uint32_t npp,
+                                           uint32_t batch, uint32_t wave, uint32_t lane) {
+  asm volatile("" : "+v"(lane));
+  const uint32_t e = lane & 7, g = 8 * task + e, b = g / npp, p = g % npp;
+  if (b >= batch) return;
+  uint8_t *dst = shards + uint64_t(b) * uint64_t(nv) * sstride + 2 * uint64_t(p);
+#pragma unroll 8
+  for (int k = 0; k < 32; ++k) {
+    const uint32_t v = (lane >> 3) + 8 * k, shard = s0 + v;
+    if (int(shard) >= nv) break;  // rows increase with k
+    *reinterpret_cast<uint16_t *>(dst + uint64_t(shard) * sstride) =
+        *reinterpret_cast<const uint16_t *>(xch + soff(v, wave) + 2 * e);
+  }
+}
+
 }  // namespace
 
 // N = n: 1024 (n_validators 766..1024) or 2048 (1025..1533); the cosets at
 // 1024 and above use LDS table image 1 (skews 1024 .. 2046, DevTables::timg)
 // at offset sh - 1024, reloaded by LDS-DMA between the two coset loops
-// PACKED (small payloads, or payload / shard pitches the 16-B path cannot
-// take): tiles run over the flattened piece space of the batch, payload b
-// owning slots [b * npp8, b * npp8 + npieces) with npp8 = pieces rounded up
-// to 8, so a wave's 8 pieces (and each 16-B chunk of a staged row) belong to
-// one payload; loads and stores take any alignment.  4096 one-piece payloads
-// are 256 tiles instead of 4096.
-template <int N, bool PACKED>
+// PK = 1, packed tiles (n = 2048 with small payloads, or payload / shard
+// pitches the 16-B path cannot take): tiles run over the flattened piece space
+// of the batch, payload b owning slots [b * npp8, b * npp8 + npieces) with
+// npp8 = pieces rounded up to 8, so a wave's 8 pieces (and each 16-B chunk of
+// a staged row) belong to one payload; loads and stores take any alignment.
+// PK = 2, packed waves (n = 1024, same cases): the waves run independently
+// over tasks of 8 consecutive pieces of the exactly flattened piece space
+// (payload b owns pieces [b * npp, (b + 1) * npp)), each staging and storing
+// its own rows (2-B stores, any payload per piece), no workgroup barrier in the
+// loop: 4096 one-piece payloads are 512 wave tasks (about 2 per CU) instead of
+// 4096 tiles (or 256 tiles of 8x-rounded slots).
+template <int N, int PK>
 __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict__ payloads,
                                                        uint64_t plen, uint64_t pstride,
                                                        uint8_t *__restrict__ shards, uint64_t slen,
@@ -399,10 +424,30 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     lds_barrier();
   };
 
+  constexpr bool PACKED = PK == 1;
   const uint64_t npieces = slen / 2;
   const uint32_t tiles_pp = uint32_t((npieces + TILE - 1) / TILE);
-  const uint64_t total = PACKED ? (uint64_t(npp8) * batch + TILE - 1) / TILE : uint64_t(tiles_pp) * batch;
-  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+  const uint64_t total = PK == 2   ? (npieces * batch + 7) / 8
+                         : PACKED ? (uint64_t(npp8) * batch + TILE - 1) / TILE
+                                  : uint64_t(tiles_pp) * batch;
+  // PK = 2: "tile" = this wave's task (a wave-uniform, scalar index)
+  const uint32_t wave_s = __builtin_amdgcn_readfirstlane(tid0 >> 6);
+  // (task t on workgroup t % grid, wave t / grid: a small batch spreads over
+  // every CU instead of filling the first ones' waves; a wave's latency, not
+  // the CU's throughput, bounds it)
+  const uint64_t first = PK == 2 ? uint64_t(wave_s) * gridDim.x + blockIdx.x : blockIdx.x;
+  const uint64_t step = PK == 2 ? uint64_t(gridDim.x) * WAVES : gridDim.x;
+  // region hand-over: a workgroup barrier (other waves read this wave's staged
+  // rows), or in PK = 2 the wave's own program order
+  const auto rsync = [&]() __attribute__((always_inline)) {
+    if constexpr (PK == 2) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      lds_barrier();
+    }
+  };
+  for (uint64_t tile = first; tile < total; tile += step) {
     // lane ids made opaque per tile: per-lane LDS addresses are recomputed in the
     // loop instead of being hoisted out of it and spilled
     uint32_t tid = tid0;
@@ -438,7 +483,13 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
       uint4 d[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if constexpr (PACKED) {
+        if constexpr (PK == 2) {
+          const uint32_t gp = uint32_t(tile) * 8 + inst * 4 * GP + g * 4 + u;  // < 2^32 (launch check)
+          const uint32_t pb = gp / uint32_t(npieces), piece = gp % uint32_t(npieces);
+          const uint64_t off = uint64_t(piece) * 2 * K + 16 * q;
+          const bool ok = pb < batch && off < plen;
+          d[u] = load16_any(payloads + uint64_t(ok ? pb : 0) * pstride + (ok ? off : 0), ok ? plen - off : 0);
+        } else if constexpr (PACKED) {
           const uint64_t piece = pw + inst * 4 * GP + g * 4 + u;
           const uint64_t off = piece * 2 * K + 16 * q;
           const bool ok = bw < batch && piece < npieces && off < plen;
@@ -470,10 +521,16 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     }
 
     // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)
-    lds_barrier();  // the other waves are done reading this region (last tile)
+    const auto store = [&](uint32_t s0) __attribute__((always_inline)) {
+      if constexpr (PK == 2)
+        store_wave(xch, shards, sstride, s0, nv, uint32_t(tile), uint32_t(npieces), batch, wave, lane);
+      else
+        store_own<PACKED>(stg, SH, sstride, s0, nv, piece0, npieces, wave, lane, tile, npp8, batch);
+    };
+    rsync();  // the other waves are done reading this region (last tile)
     stage_own(s, xch, q, inst, wave);
-    lds_barrier();
-    store_own<PACKED>(stg, SH, sstride, 0, nv, piece0, npieces, wave, lane, tile, npp8, batch);
+    rsync();
+    store(0);
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- IFFT_256 (index 0): passes A (bits 0-2), B (3-5), C (6-7)
@@ -484,7 +541,7 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
       }
     }
     ipass3(s, tabs, posA(q, 0), 0, 0);
-    lds_barrier();  // systematic rows read out of the regions
+    rsync();  // systematic rows read out of the regions
     exchange<LA, LB>(s, xch, xb);
     ipass3(s, tabs, posB(q, 0), 3, 0);
     exchange<LB, LC>(s, xch, xb);
@@ -501,14 +558,14 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
 #pragma unroll
         for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(s.l[g][r]), "+v"(s.h[g][r]));
       fpassC(s, tabs, off);
-      lds_barrier();  // previous coset's rows read out
+      rsync();  // previous coset's rows read out
       exchange<LC, LB>(s, xch, xb);
       fpass3(s, tabs, posB(q, 0), 3, off);
       exchange<LB, LA>(s, xch, xb);
       fpass3(s, tabs, posA(q, 0), 0, off);
       stage_own(s, xch, q, inst, wave);
-      lds_barrier();
-      store_own<PACKED>(stg, SH, sstride, sh, nv, piece0, npieces, wave, lane, tile, npp8, batch);
+      rsync();
+      store(sh);
       __builtin_amdgcn_sched_barrier(0);
     };
     if constexpr (N == 1024) {
@@ -539,7 +596,7 @@ bool k256_packed(size_t plen, size_t pstride, size_t batch, uintptr_t pay, uintp
 bool k256_packed_ok(size_t plen, size_t batch, uintptr_t sh, size_t sstride) {
   const size_t npp8 = ((plen + 2 * K - 1) / (2 * K) + 7) / 8 * 8;
   return sh % 2 == 0 && sstride % 2 == 0 && npp8 * batch + TILE < (size_t(1) << 32);
-}
+}  // (npp8 >= npp: also bounds the exactly flattened piece space of PK = 2)
 
 hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
@@ -549,25 +606,27 @@ hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uin
                                   reinterpret_cast<uintptr_t>(d_shards), sstride);
   if (packed && !k256_packed_ok(plen, batch, reinterpret_cast<uintptr_t>(d_shards), sstride))
     return hipErrorInvalidValue;
-  const void *fn = p.n == 1024 ? (packed ? reinterpret_cast<const void *>(&encode_k256<1024, true>)
-                                         : reinterpret_cast<const void *>(&encode_k256<1024, false>))
-                               : (packed ? reinterpret_cast<const void *>(&encode_k256<2048, true>)
-                                         : reinterpret_cast<const void *>(&encode_k256<2048, false>));
+  const void *fn = p.n == 1024 ? (packed ? reinterpret_cast<const void *>(&encode_k256<1024, 2>)
+                                         : reinterpret_cast<const void *>(&encode_k256<1024, 0>))
+                               : (packed ? reinterpret_cast<const void *>(&encode_k256<2048, 1>)
+                                         : reinterpret_cast<const void *>(&encode_k256<2048, 0>));
   if (const hipError_t e = prepare_kernel(fn, LDS_BYTES, &cus); e != hipSuccess) return e;
   const size_t sl = shard_len(p.k, plen);
   const size_t npp8 = (sl / 2 + 7) / 8 * 8;
-  const size_t tiles = packed ? (npp8 * batch + TILE - 1) / TILE : (sl / 2 + TILE - 1) / TILE * batch;
+  const size_t tiles = !packed       ? (sl / 2 + TILE - 1) / TILE * batch
+                       : p.n == 1024 ? ((sl / 2) * batch + 7) / 8  // wave tasks, spread over the CUs
+                                     : (npp8 * batch + TILE - 1) / TILE;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
 #define ECAMD_K256(NN, PK)                                                                       \
   hipLaunchKernelGGL((encode_k256<NN, PK>), dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,   \
                      uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride), \
                      int(p.nv), uint32_t(batch), uint32_t(npp8), t)
   if (p.n == 1024) {
-    if (packed) ECAMD_K256(1024, true);
-    else ECAMD_K256(1024, false);
+    if (packed) ECAMD_K256(1024, 2);
+    else ECAMD_K256(1024, 0);
   } else {
-    if (packed) ECAMD_K256(2048, true);
-    else ECAMD_K256(2048, false);
+    if (packed) ECAMD_K256(2048, 1);
+    else ECAMD_K256(2048, 0);
   }
 #undef ECAMD_K256
   return hipGetLastError();
