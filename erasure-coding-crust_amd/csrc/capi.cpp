@@ -86,7 +86,7 @@ bool encode_host(const CodeParams &p, const uint8_t *payload, size_t len, HostCt
     if (!hip_check(launch_encode(p, device_tables(d), c->h_in, len, len, 1, c->h_out, dstride,
                                  lease.ptr(), c->stream),
                    "encode launch") ||
-        !hip_check(hipStreamSynchronize(c->stream), "encode"))
+        !finish_call(c, "encode"))
       return false;
     *sl_out = sl;
     return true;
@@ -106,7 +106,7 @@ bool encode_host(const CodeParams &p, const uint8_t *payload, size_t len, HostCt
                  "encode launch") ||
       !hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost, c->stream),
                  "D2H") ||
-      !hip_check(hipStreamSynchronize(c->stream), "encode"))
+      !finish_call(c, "encode"))
     return false;
   *sl_out = sl;
   return true;
@@ -156,13 +156,13 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
                                                          "D2H"));
     // `loc` is released only after the stream has finished with it (on every
     // path: the locator cache recycles entries nobody holds)
-    const bool synced = hip_check(hipStreamSynchronize(c->stream), "reconstruct");
+    const bool synced = finish_call(c, "reconstruct");
     return launched && copied && synced;
   }
   return (direct || hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost,
                                              c->stream),
                               "D2H")) &&
-         hip_check(hipStreamSynchronize(c->stream), "reconstruct");
+         finish_call(c, "reconstruct");
 }
 
 bool take_output(HostCtx *c, size_t bytes, DataBlock *out) {
@@ -320,7 +320,7 @@ NPRSResult ECCR_reconstruct_from_systematic(unsigned long nv, const ChunksList *
                  "systematic launch") ||
       !hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost, c->stream),
                  "D2H") ||
-      !hip_check(hipStreamSynchronize(c->stream), "systematic") ||
+      !finish_call(c, "systematic") ||
       !take_output(c, out_bytes, outdata))
     return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
   return result(NPRS_RESULT_OK);

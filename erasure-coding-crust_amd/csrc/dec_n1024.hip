@@ -283,7 +283,10 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   const uint32_t tid0 = threadIdx.x, wave = tid0 >> 6;
   uint8_t *my = regions + wave * REG_BYTES;
 
-  Tabs::fill(tabs, t.mtab, 1023, [&](uint32_t i) { return uint32_t(t.skews[i]); }, tid0, THREADS);
+  // multiply tables for skew indices 0..1022: the prebuilt LDS image 0
+  // (DevTables::timg), one coalesced 80 KB copy instead of a 1023-entry gather
+  // through the skews (that gather was ~10 us of every launch; small calls pay it)
+  Tabs::copy_image<THREADS>(tabs, t.timg, tid0);
   __syncthreads();
 #ifdef DEC_STAMP
   uint64_t st_ = __builtin_amdgcn_s_memtime(), acc_[11] = {};

@@ -444,6 +444,14 @@ __global__ void __launch_bounds__(kBlock) systematic_g(const uint8_t *__restrict
   }
 }
 
+// completion signal of a per-call C-ABI call: after the call's work on the
+// stream, one lane stores `v` to a pinned host word at system scope; the host
+// spins on it (a host spin on a kernel-written flag is ~5 us faster per round
+// trip than hipStreamSynchronize: scripts/micro/launch_lat.hip)
+__global__ void signal_host(uint32_t *flag, uint32_t v) {
+  __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 int ilog2(uint32_t v) { return 31 - __builtin_clz(v); }
 
 // payload slots in gridDim.y (hardware limit 65535); the kernels loop over the rest
@@ -458,6 +466,11 @@ int groups_for(uint32_t size) {  // byte-planar groups per workgroup
 }  // namespace
 
 bool locator_wave_applicable(uint32_t n) { return n >= 64 && n <= 4096; }
+
+hipError_t launch_signal_host(uint32_t *h_flag, uint32_t v, hipStream_t s) {
+  hipLaunchKernelGGL(signal_host, dim3(1), dim3(1), 0, s, h_flag, v);
+  return hipGetLastError();
+}
 
 size_t encode_scratch_bytes(const CodeParams &p, size_t plen, size_t batch) {
   if (k1024_applicable(p)) return k1024_scratch_bytes(plen, batch);

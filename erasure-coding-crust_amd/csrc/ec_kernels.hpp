@@ -50,6 +50,8 @@ hipError_t launch_error_locator(const CodeParams &p, const uint8_t *d_present, s
 // true if launch_error_locator runs the wave-per-pattern form (64 <= n <= 4096),
 // cheap enough that a batch computes every row instead of deduplicating
 bool locator_wave_applicable(uint32_t n);
+// one-lane kernel storing v to a pinned host word (system scope, release)
+hipError_t launch_signal_host(uint32_t *h_flag, uint32_t v, hipStream_t s);
 size_t dedup_scratch_bytes(size_t batch);
 hipError_t launch_dedup_patterns(const CodeParams &p, const uint8_t *d_present, size_t batch,
                                  uint32_t *d_pattern, void *scratch, hipStream_t s);

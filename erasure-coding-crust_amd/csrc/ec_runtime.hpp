@@ -98,8 +98,16 @@ struct HostCtx {
   uint16_t *d_elog = nullptr;
   size_t d_in_cap = 0, d_out_cap = 0, d_present_cap = 0, d_elog_cap = 0;
   int device = -1;
+  uint32_t *h_flag = nullptr;  // pinned completion word (finish_call)
+  uint32_t seq = 0;
 };
 HostCtx *host_ctx();  // nullptr if no device
+// Waits until the work enqueued on c->stream is done: a signal kernel stores a
+// sequence number to the context's pinned word and the host spins on it for up
+// to kFinishSpinUs, then falls back to hipStreamSynchronize (which also
+// reports an asynchronous error).  False (error set) on a HIP error.
+constexpr double kFinishSpinUs = 200.0;
+bool finish_call(HostCtx *c, const char *what);
 bool ensure_host(uint8_t **p, size_t *cap, size_t need);
 bool ensure_dev(void **p, size_t *cap, size_t need);
 

@@ -414,7 +414,10 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
   uint8_t *stg = lds + TAB_REGION;
 
   // resident multiply tables for skew indices 0..1022 (all FFTs of k=256, n=1024)
-  Tabs::fill(tabs, t.mtab, 1023, [&](uint32_t i) { return uint32_t(t.skews[i]); }, tid0, THREADS);
+  // multiply tables for skew indices 0..1022: the prebuilt LDS image 0
+  // (DevTables::timg), one coalesced 80 KB copy instead of a 1023-entry gather
+  // through the skews (that gather was ~10 us of every launch; small calls pay it)
+  Tabs::copy_image<THREADS>(tabs, t.timg, tid0);
   __syncthreads();
   [[maybe_unused]] int img = 0;
   [[maybe_unused]] const auto load_image = [&](int q) {  // LDS-DMA: no VGPRs (the kernel is at 128)

@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <random>
 #include <string>
 #include <vector>
@@ -28,7 +29,10 @@ static double now_us() {
 }
 
 int main(int argc, char **argv) {
-  const unsigned long sizes[] = {15, 300, 5000, 100000, 1000000, 10000000};
+  // optional: argv[1] = one payload size, argv[2] = calls (traces of one size)
+  std::vector<unsigned long> sizes = {15, 300, 5000, 100000, 1000000, 10000000};
+  if (argc > 1) sizes = {std::strtoul(argv[1], nullptr, 10)};
+  const int calls = argc > 2 ? std::atoi(argv[2]) : 0;
   const unsigned long nvs[] = {6, 1024};
   for (unsigned long nv : nvs) {
     unsigned long thr = 0;
@@ -37,7 +41,7 @@ int main(int argc, char **argv) {
       std::vector<uint8_t> payload(sz);
       for (unsigned long i = 0; i < sz; ++i) payload[i] = uint8_t(97 + i % 24);
       DataBlock msg{payload.data(), sz};
-      const int reps = sz >= 10000000 ? 10 : 100;
+      const int reps = calls ? calls : sz >= 10000000 ? 10 : 100;
       // (1) the reference benchmark's call: MeasurePerformance (decode from all shards)
       unsigned long e = 0, d = 0, se = 0, sd = 0;
       for (int i = 0; i < 3; ++i) ECCR_Test_MeasurePerformance(&msg, nv, &e, &d);  // warm-up
@@ -80,7 +84,5 @@ int main(int argc, char **argv) {
       std::fflush(stdout);
     }
   }
-  (void)argc;
-  (void)argv;
   return 0;
 }
