@@ -106,7 +106,7 @@ bool encode_host(const CodeParams &p, const uint8_t *payload, size_t len, HostCt
                  "encode launch") ||
       !hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost, c->stream),
                  "D2H") ||
-      !finish_call(c, "encode"))
+      !hip_check(hipStreamSynchronize(c->stream), "encode"))
     return false;
   *sl_out = sl;
   return true;
@@ -155,14 +155,17 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
                                                                         hipMemcpyDeviceToHost, c->stream),
                                                          "D2H"));
     // `loc` is released only after the stream has finished with it (on every
-    // path: the locator cache recycles entries nobody holds)
-    const bool synced = finish_call(c, "reconstruct");
+    // path: the locator cache recycles entries nobody holds).  Kernels only
+    // (direct): the signal-kernel wait; after a D2H copy the copy-to-kernel
+    // hand-off makes that slower than waiting on the stream
+    const bool synced = direct ? finish_call(c, "reconstruct")
+                               : hip_check(hipStreamSynchronize(c->stream), "reconstruct");
     return launched && copied && synced;
   }
   return (direct || hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost,
                                              c->stream),
                               "D2H")) &&
-         finish_call(c, "reconstruct");
+         (direct ? finish_call(c, "reconstruct") : hip_check(hipStreamSynchronize(c->stream), "reconstruct"));
 }
 
 bool take_output(HostCtx *c, size_t bytes, DataBlock *out) {
@@ -320,7 +323,7 @@ NPRSResult ECCR_reconstruct_from_systematic(unsigned long nv, const ChunksList *
                  "systematic launch") ||
       !hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost, c->stream),
                  "D2H") ||
-      !finish_call(c, "systematic") ||
+      !hip_check(hipStreamSynchronize(c->stream), "systematic") ||
       !take_output(c, out_bytes, outdata))
     return result(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
   return result(NPRS_RESULT_OK);

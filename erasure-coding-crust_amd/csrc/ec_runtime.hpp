@@ -102,7 +102,8 @@ struct HostCtx {
   uint32_t seq = 0;
 };
 HostCtx *host_ctx();  // nullptr if no device
-// Waits until the work enqueued on c->stream is done: a signal kernel stores a
+// Waits until the KERNELS enqueued on c->stream are done (the small direct
+// calls, which run on pinned staging and issue no copy): a signal kernel stores a
 // sequence number to the context's pinned word and the host spins on it for up
 // to kFinishSpinUs, then falls back to hipStreamSynchronize (which also
 // reports an asynchronous error).  False (error set) on a HIP error.
