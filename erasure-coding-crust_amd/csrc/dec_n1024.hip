@@ -18,6 +18,8 @@
 //     each lane writes 8 contiguous bytes of a 512-byte output row.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "ec_device.hpp"
 #include "ec_kernels.hpp"
 
@@ -302,7 +304,12 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   const uint32_t wave_s = __builtin_amdgcn_readfirstlane(tid0 >> 6);
   // (group g on workgroup g % grid, wave g / grid: a small batch spreads over
   // every CU)
-  const uint64_t first = PACKED ? uint64_t(wave_s) * gridDim.x + blockIdx.x : blockIdx.x;
+  // big batches: a workgroup's 8 waves take 8 adjacent groups (one payload's
+  // tables shared in L1); small ones: spread, so each CU gets work
+  const bool spread = PACKED && total < uint64_t(2) * gridDim.x * WAVES;
+  const uint64_t first = !PACKED ? uint64_t(blockIdx.x)
+                         : spread ? uint64_t(wave_s) * gridDim.x + blockIdx.x
+                                  : uint64_t(blockIdx.x) * WAVES + wave_s;
   const uint64_t step = PACKED ? uint64_t(gridDim.x) * WAVES : gridDim.x;
   // m[0], m[1]: this thread's two gather slots (gather_order): row << 16 |
   // mul_index(E[row]), low half 0xFFFF = absent.  Loaded one tile ahead so the
@@ -350,9 +357,13 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     S16 s;
 
     if constexpr (PACKED) {
-      // ---- phase 1, packed: rows v = 16 lane + r (layout A) of this wave's
-      // group, flags and E[v] of the payload's pattern (decode_main:174-177);
-      // absent rows (and rows >= nv) take the zero table and read no bytes
+      // ---- phase 1, packed: this wave's group only (decode_main:174-177).
+      // The present rows (flag set, v < nv) of the payload's pattern are
+      // compacted into a list in the wave's own region (lane l reads the flags
+      // and E[v] of rows 16 l .. 16 l + 15 with three coalesced loads, a wave
+      // prefix sum places them), so the wave multiplies ceil(present / 64)
+      // rows per lane instead of 16; then the region is zeroed (absent rows)
+      // and each list entry's product is written at its row.
       const uint64_t pt = pattern ? pattern[b] : b;
       const uint32_t v0 = 16 * lane;
       const uint4 f16 = *reinterpret_cast<const uint4 *>(present + pt * N + v0);
@@ -360,36 +371,72 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       const uint4 e1 = *reinterpret_cast<const uint4 *>(elog + pt * N + v0 + 8);
       const uint32_t fw[4] = {f16.x, f16.y, f16.z, f16.w};
       const uint32_t ew[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+      uint32_t mask = 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        mask |= uint32_t(((fw[r >> 2] >> (8 * (r & 3))) & 0xFFu) != 0 && int(v0) + r < nv) << r;
+      const uint32_t cnt = __builtin_popcount(mask);
+      uint32_t incl = cnt;  // inclusive prefix sum of the counts over the lanes
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = uint32_t(__shfl_up(int(incl), d));
+        if (lane >= uint32_t(d)) incl += o;
+      }
+      const uint32_t total = uint32_t(__shfl(int(incl), 63));  // wave-uniform
+      uint32_t at = incl - cnt;
+      const uint32_t lbase = lds_addr(my);
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if ((mask >> r) & 1) {  // list entry: row << 16 | mul_index(E[row])
+          const uint32_t e = (ew[r >> 1] >> (16 * (r & 1))) & 0xFFFFu;
+          *(__attribute__((address_space(3))) uint32_t *)(uintptr_t(lbase + 4 * at)) =
+              ((v0 + r) << 16) | mul_index(e);
+          ++at;
+        }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t nj = (total + 63) / 64;  // list entries per lane (uniform)
+      uint32_t ent[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        ent[j] = uint32_t(j) < nj && lane + 64 * j < total
+                     ? *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t(lbase + 4 * (lane + 64 * j)))
+                     : 0xFFFFu;  // no entry: the zero table, no bytes read
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) lds_st2(lbase | raddr(v0 + r), make_uint2(0, 0));  // absent rows
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
       const uint64_t cg = 4 * uint64_t(uint32_t(tile) % gpp);
       const uint64_t have = ncols - cg;  // columns of the group inside the payload
       const uint32_t avail = have >= 4 ? 8u : uint32_t(2 * have);
-      const uint8_t *rowp = SH + uint64_t(v0) * sstride + 2 * cg;
+      const uint8_t *colp = SH + 2 * cg;
       // rows 8-B aligned and the group whole: one 8-B load per row (uniform)
-      const bool wide = avail == 8 && ((sstride | reinterpret_cast<uintptr_t>(rowp)) & 7) == 0;
+      const bool wide = avail == 8 && ((sstride | reinterpret_cast<uintptr_t>(colp)) & 7) == 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {  // 4 rows at a time: 4 tables + 4 rows in flight
+      for (int q = 0; q < 4; ++q) {  // 4 entries at a time: 4 tables + 4 rows in flight
+        if (uint32_t(4 * q) >= nj) break;  // uniform
         Tab T[4];
         uint2 d[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int r = 4 * q + i;
-          const bool on = (fw[r >> 2] >> (8 * (r & 3))) & 0xFFu && int(v0) + r < nv;
-          const uint32_t e = (ew[r >> 1] >> (16 * (r & 1))) & 0xFFFFu;
-          load_tab(t.mtab, on ? mul_index(e) : 65535u, T[i]);  // mtab[65535] = * 0
+          const uint32_t m = ent[4 * q + i], v = m >> 16;
+          const bool on = (m & 0xFFFFu) != 0xFFFFu;
+          load_tab(t.mtab, on ? (m & 0xFFFFu) : 65535u, T[i]);  // mtab[65535] = * 0
           d[i] = make_uint2(0, 0);
-          if (on) d[i] = wide ? *reinterpret_cast<const uint2 *>(rowp + uint64_t(r) * sstride)
-                              : load8_any(rowp + uint64_t(r) * sstride, avail);
+          if (on) d[i] = wide ? *reinterpret_cast<const uint2 *>(colp + uint64_t(v) * sstride)
+                              : load8_any(colp + uint64_t(v) * sstride, avail);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int r = 4 * q + i;
-          if (v0 + r < uint32_t(K)) *reinterpret_cast<uint2 *>(stage + stage_addr(v0 + r, wave)) = d[i];
+          const uint32_t m = ent[4 * q + i], v = m >> 16;
+          if ((m & 0xFFFFu) == 0xFFFFu) continue;
+          if (v < uint32_t(K)) *reinterpret_cast<uint2 *>(stage + stage_addr(v, wave)) = d[i];
           const uint32_t xh = vperm(d[i].y, d[i].x, 0x06040200u), xl = vperm(d[i].y, d[i].x, 0x07050301u);
           uint32_t l = 0, h = 0;
           mul_acc(xl, xh, T[i], l, h);
-          // into the wave's own region (layout A, read back below): keeps the
-          // register live ranges those of the unpacked kernel
-          *reinterpret_cast<uint2 *>(my + raddr(v0 + r)) = make_uint2(l, h);
+          lds_st2(lbase | raddr(v), make_uint2(l, h));  // layout A, read back below
         }
         __builtin_amdgcn_sched_barrier(0);  // one batch of tables live at a time
       }
@@ -739,7 +786,12 @@ hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
                                     size_t batch, uint8_t *d_out, size_t ostride, void *scratch,
                                     hipStream_t s) {
   int cus = 0;
-  const bool packed = n1024_packed(slen, reinterpret_cast<uintptr_t>(d_shards), sstride);
+  // ECCR_AMD_RECON_PACKED=1 (experiments, scripts/ab_*): packed at every size
+  static const bool force_packed = [] {
+    const char *e = std::getenv("ECCR_AMD_RECON_PACKED");
+    return e && e[0] == '1';
+  }();
+  const bool packed = force_packed || n1024_packed(slen, reinterpret_cast<uintptr_t>(d_shards), sstride);
   const size_t ncols4 = (slen / 2 + 3) / 4 * 4;
   if (packed && (reinterpret_cast<uintptr_t>(d_shards) % 2 != 0 || sstride % 2 != 0 ||
                  ncols4 * batch + COLS >= (size_t(1) << 32)))
