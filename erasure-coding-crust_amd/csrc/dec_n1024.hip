@@ -496,7 +496,11 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       }
 #pragma unroll
       for (int g = 0; g < 8; ++g)
+#ifdef DEC_DIAG_GATHER  // diagnostic builds only (wrong results): conflict-free gather writes
+        *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(tid + half * THREADS)) = make_uint2(l[g], h[g]);
+#else
         *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l[g], h[g]);
+#endif
     }
     }
     if (tile + step < total) load_meta(tile + step, tid, meta_next);
