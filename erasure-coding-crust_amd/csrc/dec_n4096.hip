@@ -123,42 +123,38 @@ reconstruct_n4096(
     const auto has = [&](int half) { return (mq[half] & 0xffffu) != 0xffffu; };
 
     // ---- IFFT quarters 3, 2, 1, 0 (quarter 0's tables stay for the FFT), each
-    // folded into P and Qa as soon as it is transformed
-    const auto quarter = [&](const int q) __attribute__((always_inline)) {
+    // folded into P and Qa as soon as it is transformed.  A quarter's table
+    // image is requested (LDS-DMA) as soon as every wave is done with the
+    // previous quarter's IFFT, so it lands behind that quarter's accumulation
+    // and this quarter's row gather; the first gather row and its E[v] table
+    // are requested before that barrier (registers only).
+    uint32_t w0[16];  // this thread's first gather slot of the next quarter
+    Tab RT0;
+    const uint64_t avail = slen - 2 * col0;
+    const auto load_row = [&](const int q, const int half, uint32_t (&w)[16], Tab &RT) __attribute__((always_inline)) {
+      const uint8_t *row = SH + uint64_t(1024 * q + (mq[half] >> 16)) * sstride + 2 * col0;
+      if (avail >= 64) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint4 d = reinterpret_cast<const uint4 *>(row)[j];
+          w[4 * j] = d.x;
+          w[4 * j + 1] = d.y;
+          w[4 * j + 2] = d.z;
+          w[4 * j + 3] = d.w;
+        }
+      } else {
+        load_row_tail64(row, avail, w);
+      }
+      load_tab(t.mtab, mq[half] & 0xffffu, RT);
+    };
+    const auto quarter = [&](const int q, const int qnext) __attribute__((always_inline)) {
       S16 Qq;
       __builtin_amdgcn_sched_barrier(0);
       uint32_t tq = tid;
       asm volatile("" : "+v"(tq));  // this quarter's addresses and loads are not hoisted above here
       const uint32_t lq = tq & 63;
       // gather + scale the quarter's present rows (decode_main:174-177) into
-      // the 8 groups' regions: thread -> rows 1024q + tid, + 512.  The first
-      // row and its E[v] table are requested before the barrier (registers
-      // only), so their latency overlaps the wait for the other waves.
-      uint32_t w[1024 / THREADS][16];
-      Tab RT[1024 / THREADS];
-      const uint64_t avail = slen - 2 * col0;
-      const auto load_row = [&](int half) __attribute__((always_inline)) {
-        const uint8_t *row = SH + uint64_t(1024 * q + (mq[half] >> 16)) * sstride + 2 * col0;
-        if (avail >= 64) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint4 d = reinterpret_cast<const uint4 *>(row)[j];
-            w[half][4 * j] = d.x;
-            w[half][4 * j + 1] = d.y;
-            w[half][4 * j + 2] = d.z;
-            w[half][4 * j + 3] = d.w;
-          }
-        } else {
-          load_row_tail64(row, avail, w[half]);
-        }
-        load_tab(t.mtab, mq[half] & 0xffffu, RT[half]);
-      };
-      if (has(0)) load_row(0);
-      lds_barrier();  // every wave is done with the tables and its region
-      // the quarter's tables (skews 1024q + i) by LDS-DMA, in the background
-      // of the row gather; retired before the barrier below
-      Tabs::dma_image<THREADS>(tabs, t.timg + q * kTabImageBytes, tq);
-      __builtin_amdgcn_sched_barrier(0);
+      // the 8 groups' regions: thread -> rows 1024q + tid, + 512
 #pragma unroll
       for (int half = 0; half < 1024 / THREADS; ++half) {
         const uint32_t vl = mq[half] >> 16;
@@ -166,19 +162,23 @@ reconstruct_n4096(
 #pragma unroll
         for (int g = 0; g < 8; ++g) l[g] = h[g] = 0;
         if (has(half)) {
-          if (half > 0) load_row(half);
+          uint32_t w1[16];
+          Tab RT1;
+          if (half > 0) load_row(q, half, w1, RT1);
+          const uint32_t *w = half > 0 ? w1 : w0;
+          const Tab &RT = half > 0 ? RT1 : RT0;
 #pragma unroll
           for (int g = 0; g < 8; ++g) {
-            const uint32_t a = w[half][2 * g], c = w[half][2 * g + 1];
+            const uint32_t a = w[2 * g], c = w[2 * g + 1];
             const uint32_t xh = vperm(c, a, 0x06040200u), xl = vperm(c, a, 0x07050301u);
-            mul_acc(xl, xh, RT[half], l[g], h[g]);
+            mul_acc(xl, xh, RT, l[g], h[g]);
           }
         }
 #pragma unroll
         for (int g = 0; g < 8; ++g)
           *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(vl)) = make_uint2(l[g], h[g]);
       }
-      if (q > 0) load_meta(q - 1, tq);
+      if (qnext >= 0) load_meta(qnext, tq);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // table image landed
       lds_barrier();
       __builtin_amdgcn_sched_barrier(0);
@@ -196,6 +196,12 @@ reconstruct_n4096(
       if (q == 0) ifft1024<true>(Qq, tabs, my, lq);  // -> layout C; quarter 0 is at index 0
       else ifft1024<false>(Qq, tabs, my, lq);
       __builtin_amdgcn_sched_barrier(0);
+      if (qnext >= 0) {  // the next quarter's first row and tables
+        if (has(0)) load_row(qnext, 0, w0, RT0);
+        lds_barrier();  // every wave is done with this quarter's tables and its region
+        Tabs::dma_image<THREADS>(tabs, t.timg + qnext * kTabImageBytes, tq);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       // P += p_q u_q, Qa += k_q u_q.  The constants are mostly 0 or 1 (the
       // skews at 1023 and 2047 are 0xFFFF: n = 4096 gives p = (1, 0, 0, 0),
       // k = (0, 1, 1 + s, s); n = 2048 p = (1, 0), k = (1, 1)), so each is a
@@ -241,13 +247,17 @@ reconstruct_n4096(
     for (int r = 0; r < 16; ++r) P.l[r] = P.h[r] = Qa.l[r] = Qa.h[r] = 0;
     // a quarter wholly at or above n_validators holds no received symbol: its
     // IFFT is zero and adds nothing (n = 4096 with n_validators <= 3072)
-    load_meta(NQ == 4 && 3 * 1024 < nv ? 3 : NQ == 4 ? 2 : 1, tid);
+    const int qfirst = NQ == 4 && 3 * 1024 < nv ? 3 : NQ == 4 ? 2 : 1;
+    load_meta(qfirst, tid);
+    if (has(0)) load_row(qfirst, 0, w0, RT0);
+    lds_barrier();  // every wave is done with the last tile's output tables and its region
+    Tabs::dma_image<THREADS>(tabs, t.timg + qfirst * kTabImageBytes, tid);
     if constexpr (NQ == 4) {
-      if (3 * 1024 < nv) quarter(3);
-      quarter(2);
+      if (3 * 1024 < nv) quarter(3, 2);
+      quarter(2, 1);
     }
-    quarter(1);
-    quarter(0);
+    quarter(1, 0);
+    quarter(0, -1);
 
     // ---- cross-quarter IFFT stages (10, 11), the quarter bits of the formal
     // derivative and FFT stages 11 / 10 on the side that reaches y < 1024 are

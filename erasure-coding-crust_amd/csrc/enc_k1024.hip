@@ -4,14 +4,10 @@
 // encodeLow (poly_encoder.hpp:217-240) for k = 1024 is one IFFT_1024 and up to
 // three FFT_1024 at coset shifts 1024 / 2048 / 3072, each with its own 1023
 // skews (80 KB of multiply tables).  All 4095 tables do not fit LDS next to the
-// exchange regions, so the encode runs as one launch per transform, each with
-// its transform's tables resident for the whole (persistent) launch:
-//   launch 0: payload -> systematic shards 0..1023, IFFT -> coefficients,
-//             written to a device scratch in the kernel's register order;
-//   launch s (s = 1024, 2048, 3072 < nv): coefficients -> FFT -> shards
-//             [s, s + 1024).
-// The scratch round trip adds 4 x payload bytes of HBM traffic to a VALU-bound
-// kernel.
+// exchange regions, so one persistent launch cycles the four table sets
+// through LDS per tile (LDS-DMA, hidden behind shard stores; see the kernel).
+// (Until round 3: one launch per transform with the coefficients round-tripped
+// through HBM)
 //
 // Tile = 64 consecutive pieces (piece = 2048 payload bytes = 1024 symbols);
 // wave w owns pieces [8w, 8w + 8) as two byte-planar groups of 4, each run
@@ -19,6 +15,8 @@
 // are staged in two halves of 512 rows through the waves' own regions and
 // stored as 16 B per lane, 128-B row segments.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 #include "ec_kernels.hpp"
 #include "tf1024.hpp"
@@ -33,7 +31,8 @@ constexpr int THREADS = 64 * WAVES;
 constexpr int TILE = 8 * WAVES;  // pieces
 constexpr int LDS_BYTES = Tabs::kBytes + WAVES * REG_BYTES;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
-constexpr size_t SCRATCH_PER_TILE = size_t(WAVES) * 2 * 16 * 64 * sizeof(uint2);
+constexpr size_t SCRATCH_PER_WG = size_t(WAVES) * 2 * 16 * 64 * sizeof(uint2);  // a tile's coefficients
+constexpr size_t kMaxGrid = 1024;  // workgroups of the launch (>= the CU count)
 
 // own-region staging slot of row v (0..511) of wave w: the 8 lanes reading one
 // row from the 8 regions hit 8 distinct 16-B slots
@@ -115,24 +114,33 @@ __device__ __forceinline__ void load_group(S16 &s, const uint8_t *P, uint64_t pl
   }
 }
 
-__device__ __forceinline__ uint2 *coef_at(uint2 *scratch, uint64_t tile, uint32_t wave, int g) {
-  return scratch + ((tile * WAVES + wave) * 2 + uint64_t(g)) * (16 * 64);
+// workgroup wg's coefficient slot, wave w, group g: 16 registers x 64 lanes
+__device__ __forceinline__ uint2 *coef_at(uint2 *scratch, uint64_t wg, uint32_t wave, int g) {
+  return scratch + ((wg * WAVES + wave) * 2 + uint64_t(g)) * (16 * 64);
 }
 
-// MODE 0: IFFT launch (shift 0); MODE 1: FFT launch at coset `shift`
-template <int MODE>
+// One persistent launch for all four transforms.  The four 80 KB table sets
+// take turns in LDS, loaded by LDS-DMA: coset 2's, coset 3's and the next
+// tile's index-0 set behind the previous coset's shard stores (its tables are
+// no longer read by then), coset 1's right after the IFFT.  Coset 1 takes the
+// IFFT coefficients from the registers; cosets 2 and 3 read them back from a
+// per-workgroup scratch slot (128 KB, rewritten every tile, so it stays in L2
+// / the memory-side cache).  (Prefetching them behind the previous coset's
+// stores needs 64 more VGPRs at the 256 limit: 15 spills, 7.61 vs 6.95 ms.)
 __global__ void __launch_bounds__(THREADS)
-    encode_k1024(const uint8_t *__restrict__ payloads, uint64_t plen, uint64_t pstride,
-                 uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride, int nv,
-                 uint32_t batch, uint32_t shift, uint2 *__restrict__ coef, DevTables t) {
+    encode_k1024_fused(const uint8_t *__restrict__ payloads, uint64_t plen, uint64_t pstride,
+                       uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride, int nv,
+                       uint32_t batch, uint2 *__restrict__ coef, DevTables t) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
   uint8_t *regions = lds + Tabs::kBytes;
   const uint32_t tid0 = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid0 >> 6);
   uint8_t *my = regions + wave * REG_BYTES;
+  // cosets 1 .. ncos - 1 start below n_validators (poly_encoder.hpp:229-236)
+  const uint32_t ncos = uint32_t(nv + K - 1) / K;
+  uint2 *const cw0 = coef_at(coef, blockIdx.x, wave, 0), *const cw1 = coef_at(coef, blockIdx.x, wave, 1);
 
-  // this transform's 1023 skews (additive_fft.hpp:108,126: skews[j - 1 + index])
-  Tabs::copy_image<THREADS>(tabs, t.timg + (shift / K) * kTabImageBytes, tid0);
+  Tabs::copy_image<THREADS>(tabs, t.timg, tid0);  // index 0 (the IFFT)
   __syncthreads();
 
   const uint64_t npieces = slen / 2;
@@ -145,39 +153,48 @@ __global__ void __launch_bounds__(THREADS)
     const uint64_t b = tile / tiles_pp;
     const uint64_t piece0 = (tile % tiles_pp) * TILE;
     uint8_t *SH = shards + b * uint64_t(nv) * sstride;
+    const uint8_t *P = payloads + b * pstride;
     S16 g0, g1;
-    if constexpr (MODE == 0) {
-      const uint8_t *P = payloads + b * pstride;
-      load_group(g0, P, plen, piece0 + 8 * wave, lane);
-      load_group(g1, P, plen, piece0 + 8 * wave + 4, lane);
-      // systematic shards 0..1023 = the data symbols (poly_encoder.hpp:239)
+    const auto load_coef = [&]() __attribute__((always_inline)) {
+      // opaque addresses: the values stored after the IFFT must be read back,
+      // not forwarded from the registers (which would stay live meanwhile)
+      const uint2 *r0 = cw0, *r1 = cw1;
+      asm volatile("" : "+s"(r0), "+s"(r1));
 #pragma unroll
-      for (uint32_t hf = 0; hf < 2; ++hf) {
-        lds_barrier();  // the other waves are done reading the regions
-        stage_half(g0, g1, my, lane, wave, hf);
-        lds_barrier();
-        store_half(regions, SH, sstride, 512 * hf, nv, piece0, npieces, wave, lane);
+      for (int r = 0; r < 16; ++r) {
+        const uint2 x = r0[r * 64 + lane], y = r1[r * 64 + lane];
+        g0.l[r] = x.x;
+        g0.h[r] = x.y;
+        g1.l[r] = y.x;
+        g1.h[r] = y.y;
       }
+    };
+    load_group(g0, P, plen, piece0 + 8 * wave, lane);
+    load_group(g1, P, plen, piece0 + 8 * wave + 4, lane);
+    // systematic shards 0..1023 = the data symbols (poly_encoder.hpp:239)
+#pragma unroll
+    for (uint32_t hf = 0; hf < 2; ++hf) {
+      lds_barrier();  // the other waves are done reading the regions
+      stage_half(g0, g1, my, lane, wave, hf);
       lds_barrier();
-      ifft1024<true>(g0, tabs, my, lane);  // index 0 (zero skews at the top stages)
-      ifft1024<true>(g1, tabs, my, lane);
-      uint2 *c0 = coef_at(coef, tile, wave, 0), *c1 = coef_at(coef, tile, wave, 1);
+      store_half(regions, SH, sstride, 512 * hf, nv, piece0, npieces, wave, lane);
+    }
+    // the index-0 tables (the last tile's DMA) landed; the regions are free
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    ifft1024<true>(g0, tabs, my, lane);
+    ifft1024<true>(g1, tabs, my, lane);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        c0[r * 64 + lane] = make_uint2(g0.l[r], g0.h[r]);
-        c1[r * 64 + lane] = make_uint2(g1.l[r], g1.h[r]);
-      }
-    } else {
-      const uint2 *c0 = coef_at(coef, tile, wave, 0), *c1 = coef_at(coef, tile, wave, 1);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const uint2 a = c0[r * 64 + lane], bb = c1[r * 64 + lane];
-        g0.l[r] = a.x;
-        g0.h[r] = a.y;
-        g1.l[r] = bb.x;
-        g1.h[r] = bb.y;
-      }
-      lds_barrier();  // the other waves are done reading this region (last tile)
+    for (int r = 0; r < 16; ++r) {  // read back by cosets 2 and 3 (coset 1 uses the registers)
+      cw0[r * 64 + lane] = make_uint2(g0.l[r], g0.h[r]);
+      cw1[r * 64 + lane] = make_uint2(g1.l[r], g1.h[r]);
+    }
+    lds_barrier();  // every wave is done with the index-0 tables
+    Tabs::dma_image<THREADS>(tabs, t.timg + kTabImageBytes, tid);
+    const auto coset = [&](const uint32_t s) __attribute__((always_inline)) {
+      if (s > 1) load_coef();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // coset s's tables and coefficients landed
+      lds_barrier();  // (all waves' slices) and the regions are free
       fft1024(g0, tabs, my, lane);
       fft1024(g1, tabs, my, lane);
 #pragma unroll
@@ -185,10 +202,16 @@ __global__ void __launch_bounds__(THREADS)
         if (hf) lds_barrier();
         stage_half(g0, g1, my, lane, wave, hf);
         lds_barrier();
-        store_half(regions, SH, sstride, shift + 512 * hf, nv, piece0, npieces, wave, lane);
+        if (hf == 0)  // every wave is past its FFT: the next set (index 0 after the last coset)
+          Tabs::dma_image<THREADS>(tabs, t.timg + (s + 1 < ncos ? s + 1 : 0) * kTabImageBytes, tid);
+        store_half(regions, SH, sstride, s * K + 512 * hf, nv, piece0, npieces, wave, lane);
       }
-    }
+    };
+    coset(1);
+    coset(2);
+    if (ncos > 3) coset(3);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
 }
 
 }  // namespace
@@ -196,29 +219,24 @@ __global__ void __launch_bounds__(THREADS)
 bool k1024_applicable(const CodeParams &p) { return p.k == 1024 && p.n == 4096; }
 
 size_t k1024_scratch_bytes(size_t plen, size_t batch) {
-  const size_t pieces = shard_len(K, plen) / 2;
-  return (pieces + TILE - 1) / TILE * batch * SCRATCH_PER_TILE;
+  const size_t tiles = (shard_len(K, plen) / 2 + TILE - 1) / TILE * batch;
+  return std::min(tiles, kMaxGrid) * SCRATCH_PER_WG;  // one coefficient slot per workgroup
 }
 
 hipError_t launch_encode_k1024(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                                size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                                size_t sstride, void *scratch, hipStream_t s) {
   int cus = 0;
-  for (const void *f : {reinterpret_cast<const void *>(&encode_k1024<0>),
-                        reinterpret_cast<const void *>(&encode_k1024<1>)})
-    if (const hipError_t e = prepare_kernel(f, LDS_BYTES, &cus); e != hipSuccess) return e;
-  if (!scratch) return hipErrorInvalidValue;
   const size_t sl = shard_len(p.k, plen);
   const size_t tiles = (sl / 2 + TILE - 1) / TILE * batch;
-  const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
-  uint2 *coef = static_cast<uint2 *>(scratch);
-  hipLaunchKernelGGL(encode_k1024<0>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
+  if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&encode_k1024_fused), LDS_BYTES, &cus);
+      e != hipSuccess)
+    return e;
+  const unsigned grid = unsigned(std::min({tiles, size_t(cus), kMaxGrid}));
+  if (!scratch) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(encode_k1024_fused, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
                      uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride),
-                     int(p.nv), uint32_t(batch), 0u, coef, t);
-  for (uint32_t sh = K; sh < p.n && sh < p.nv; sh += K)
-    hipLaunchKernelGGL(encode_k1024<1>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
-                       uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride),
-                       int(p.nv), uint32_t(batch), sh, coef, t);
+                     int(p.nv), uint32_t(batch), static_cast<uint2 *>(scratch), t);
   return hipGetLastError();
 }
 
