@@ -76,6 +76,25 @@ Lin n4096_lin(int nq) {
   return lin;
 }
 
+// Per payload, the LDS image (LdsTabs<1024> layout, as DevTables::timg) of
+// its output tables E[y], y < 1024 (decode_main:185-188): the k = 1024
+// reconstruct fills its output tables with one linear LDS-DMA per tile
+// instead of a per-tile gather of 1024 indexed 80-byte tables (two dependent
+// global latencies).  Chunk i of the image is plane i / 1024, slot i % 1024 of
+// entry y = (slot & ~15) | f with LdsTabs::addr's swizzle f inverted.
+__global__ void __launch_bounds__(256)
+    n4096_out_image(const uint16_t *__restrict__ elog, const uint32_t *__restrict__ pattern, int n,
+                    const MulTab *__restrict__ mtab, uint8_t *__restrict__ img) {
+  const uint64_t b = blockIdx.x;
+  const uint16_t *E = elog + (pattern ? pattern[b] : b) * uint64_t(n);
+  uint4 *dst = reinterpret_cast<uint4 *>(img + b * kTabImageBytes);
+  for (uint32_t i = threadIdx.x; i < 5 * 1024; i += 256) {
+    const uint32_t q = i >> 10, sl = i & 1023;
+    const uint32_t y = (sl & ~15u) | ((sl ^ (sl >> 4) ^ (sl >> 8)) & 15u);
+    dst[i] = reinterpret_cast<const uint4 *>(mtab + mul_index(E[y]))[q];
+  }
+}
+
 }  // namespace
 
 // NQ = n / 1024 quarters (2 or 4); K = k = 2^KB (256, 512 or 1024)
@@ -86,7 +105,7 @@ reconstruct_n4096(
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
     const uint32_t *__restrict__ pattern, const uint32_t *__restrict__ order,
     uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t K, uint32_t batch,
-    DevTables t, Lin lin) {
+    DevTables t, Lin lin, const uint8_t *__restrict__ oimg) {
   constexpr int N = 1024 * NQ;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
@@ -288,9 +307,12 @@ reconstruct_n4096(
     // scaled by E[y] (tables now in LDS), present y copied from the shard
     const uint64_t cbase = col0 + 4 * wave;
     lds_barrier();  // every wave is done with the FFT tables
-    if constexpr (KB == 10)  // all 1024: skipping the present y measured 3% slower here
-      Tabs::gather<THREADS>(tabs, t.mtab, [&](uint32_t y) { return mul_index(E[y]); }, tid);
-    else  // k = 256 / 512: the erased y < k only (nv = 2500 3.32 -> 3.20 ms per 512 x 1 MB)
+    if constexpr (KB == 10) {  // all 1024, from this payload's prebuilt image (n4096_out_image)
+      __builtin_amdgcn_sched_barrier(0);
+      Tabs::dma_image<THREADS>(tabs, oimg + b * kTabImageBytes, tid);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    } else  // k = 256 / 512: the erased y < k only (nv = 2500 3.32 -> 3.20 ms per 512 x 1 MB)
       Tabs::gather_if<THREADS>(
           tabs, t.mtab, [&](uint32_t y) { return mul_index(E[y]); },
           [&](uint32_t y) { return y < K; }, [&](uint32_t y) { return !(int(y) < nv && pr[y]); }, tid);
@@ -384,6 +406,10 @@ reconstruct_n4096(
   }
 }
 
+size_t n4096_scratch_bytes(const CodeParams &p, size_t batch) {
+  return gather_order_bytes(p, batch) + (p.k == 1024 ? batch * kTabImageBytes : 0);
+}
+
 bool n4096_applicable(const CodeParams &p) {  // the (n, k) instantiated below
   return (p.n == 4096 && (p.k == 1024 || p.k == 512)) || (p.n == 2048 && (p.k == 512 || p.k == 256));
 }
@@ -402,10 +428,14 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
                        : reinterpret_cast<const void *>(&reconstruct_n4096<2, 8>);
   if (const hipError_t e = prepare_kernel(fn, LDS_BYTES, &cus); e != hipSuccess) return e;
   if (!scratch) return hipErrorInvalidValue;
-  uint32_t *order = static_cast<uint32_t *>(scratch);  // gather_order_bytes(p, batch)
+  uint32_t *order = static_cast<uint32_t *>(scratch);  // n4096_scratch_bytes(p, batch)
   if (const hipError_t e = launch_gather_order(p, d_present, d_err_log, d_pattern, batch, order, s);
       e != hipSuccess)
     return e;
+  uint8_t *oimg = static_cast<uint8_t *>(scratch) + gather_order_bytes(p, batch);
+  if (p.k == 1024)
+    hipLaunchKernelGGL(n4096_out_image, dim3(unsigned(batch)), dim3(256), 0, s, d_err_log, d_pattern,
+                       int(p.n), t.mtab, oimg);
   const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   static const Lin lin4 = n4096_lin(4), lin2 = n4096_lin(2);
@@ -414,7 +444,7 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
     hipLaunchKernelGGL((reconstruct_n4096<NQv, KBv>), dim3(grid), dim3(THREADS), LDS_BYTES, s,   \
                        d_shards, uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, order, d_out, \
                        uint64_t(ostride), int(p.nv), uint32_t(p.k), uint32_t(batch), t,         \
-                       NQv == 4 ? lin4 : lin2);
+                       NQv == 4 ? lin4 : lin2, oimg);
   ECAMD_D4(4, 10)
   else ECAMD_D4(4, 9)
   else ECAMD_D4(2, 9)

@@ -190,12 +190,16 @@ struct LdsTabs {
                                                    uint32_t tid) {
     constexpr int kChunks = kBytes / 16;
     static_assert(kChunks % THREADS == 0 && THREADS % 64 == 0, "whole chunks per thread");
-    const uint32_t wave_base = (tid & ~63u) * 16;  // this wave's 1 KB slice
+    // wave-uniform source / destination (SGPRs) + one per-lane byte offset:
+    // no per-chunk address registers for the compiler to keep live between calls
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t loff = (tid & 63) * 16;
 #pragma unroll
-    for (int k = 0; k < kChunks / THREADS; ++k)
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void *)(img + 16 * (tid + k * THREADS)),
-          (__attribute__((address_space(3))) void *)(base + wave_base + k * THREADS * 16), 16, 0, 0);
+    for (int k = 0; k < kChunks / THREADS; ++k) {
+      const uint32_t off = (uint32_t(k) * THREADS + wave * 64) * 16;  // this wave's 1 KB slice
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(img + off + loff),
+                                       (__attribute__((address_space(3))) void *)(base + off), 16, 0, 0);
+    }
   }
   // cooperative gather of ENTRIES tables, entry i <- mtab[src(i)], all index
   // loads then all table loads in flight at once

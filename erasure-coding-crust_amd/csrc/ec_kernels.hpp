@@ -112,8 +112,9 @@ hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
                                     const uint32_t *d_pattern, size_t batch, uint8_t *d_out,
                                     size_t ostride, void *scratch, hipStream_t s);
 
-// specialised kernels (dec_n4096.hip); scratch: gather_order_bytes(p, batch)
+// specialised kernels (dec_n4096.hip); scratch: n4096_scratch_bytes(p, batch)
 bool n4096_applicable(const CodeParams &p);
+size_t n4096_scratch_bytes(const CodeParams &p, size_t batch);
 hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
                                     const uint8_t *d_shards, size_t slen, size_t sstride,
                                     const uint8_t *d_present, const uint16_t *d_err_log,
