@@ -84,6 +84,14 @@ __device__ __forceinline__ uint32_t skew_idx(uint32_t pos_a, int m) {
   return (pos_a & ~(2 * d - 1)) + d - 1;  // FFT index 0 (poly_encoder.hpp:180,183)
 }
 
+// skew index at stage 2 whose element equals the skew element of position
+// pos_a at stage m (2 (pos_a >> (m + 1)), additive_fft.hpp:47-97 with the Cantor
+// relabelling: skews[i] = log(((i + 1) >> ctz(i + 1)) - 1)): that element is
+// < 256 iff the result is < 1024, and its image slot holds a subfield table
+__device__ __forceinline__ uint32_t sub_alias(uint32_t pos_a, int m) {
+  return ((pos_a >> (m + 1)) << 3) | 3u;
+}
+
 struct S16 {
   uint32_t l[16], h[16];
 };
@@ -92,6 +100,11 @@ __device__ __forceinline__ void ib(S16 &s, int a, int b, const Tab &T) {
   s.l[b] ^= s.l[a];
   s.h[b] ^= s.h[a];
   mul_acc(s.l[b], s.h[b], T, s.l[a], s.h[a]);
+}
+__device__ __forceinline__ void ib(S16 &s, int a, int b, const SubTab &T) {
+  s.l[b] ^= s.l[a];
+  s.h[b] ^= s.h[a];
+  mul_acc_sub(s.l[b], s.h[b], T, s.l[a], s.h[a]);
 }
 
 // GF(2)-linear part of the swizzled table address (LdsTabs::addr minus the
@@ -105,14 +118,26 @@ __host__ __device__ constexpr uint32_t tlin(uint32_t idx) {
 __device__ __forceinline__ void tab_at(const uint8_t *, uint32_t lin, Tab &T) {
   lds_tab_abs<Tabs::kPlane>(lin, T);
 }
+// the data runs in tower coordinates and the tables are tower
+// image 0: stages >= tower_sub_min(0) = 2 hold subfield tables
+__device__ __forceinline__ void tab_at(const uint8_t *, uint32_t lin, SubTab &T) {
+  lds_subtab_abs<Tabs::kPlane>(lin, T);
+}
+constexpr int SUB = tower_sub_min(0);
 
 // inverse radix-16 pass over position bits b0..b0+3: pos(r) = lane part | (r << b0),
 // lb = tlin(lane part).  15 tables (8 + 4 + 2 + 1), each requested one step
 // ahead of its use so a table load is always in flight behind the multiplies.
 template <int B0>
 __device__ __forceinline__ void ipass4(S16 &s, const uint8_t *tabs, uint32_t lb) {
-  Tab T[2];
-  tab_at(tabs, lb ^ tlin(skew_idx(0, B0)), T[0]);
+  Tab T[2];      // stages < SUB: general tables
+  SubTab U[2];   // stages >= SUB: subfield tables
+  const auto fetch = [&](int t, int blk, int slot) __attribute__((always_inline)) {
+    const uint32_t a = lb ^ tlin(skew_idx(uint32_t(blk) << B0, B0 + t));
+    if (B0 + t >= SUB) tab_at(tabs, a, U[slot]);
+    else tab_at(tabs, a, T[slot]);
+  };
+  fetch(0, 0, 0);
   int k = 0;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -120,9 +145,12 @@ __device__ __forceinline__ void ipass4(S16 &s, const uint8_t *tabs, uint32_t lb)
 #pragma unroll
     for (int blk = 0; blk < 16; blk += 2 * d, ++k) {  // one skew per block of 2d registers
       const int nt = blk + 2 * d < 16 ? t : t + 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
-      if (nt < 4) tab_at(tabs, lb ^ tlin(skew_idx(uint32_t(nblk) << B0, B0 + nt)), T[(k + 1) & 1]);
+      if (nt < 4) fetch(nt, nblk, (k + 1) & 1);
 #pragma unroll
-      for (int i = 0; i < d; ++i) ib(s, blk + i, blk + i + d, T[k & 1]);
+      for (int i = 0; i < d; ++i) {
+        if (B0 + t >= SUB) ib(s, blk + i, blk + i + d, U[k & 1]);
+        else ib(s, blk + i, blk + i + d, T[k & 1]);
+      }
     }
   }
 }
@@ -288,7 +316,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   // multiply tables for skew indices 0..1022: the prebuilt LDS image 0
   // (DevTables::timg), one coalesced 80 KB copy instead of a 1023-entry gather
   // through the skews (that gather was ~10 us of every launch; small calls pay it)
-  Tabs::copy_image<THREADS>(tabs, t.timg, tid0);
+  Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);
   __syncthreads();
 #ifdef DEC_STAMP
   uint64_t st_ = __builtin_amdgcn_s_memtime(), acc_[11] = {};
@@ -423,7 +451,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         for (int i = 0; i < 4; ++i) {
           const uint32_t m = ent[4 * q + i], v = m >> 16;
           const bool on = (m & 0xFFFFu) != 0xFFFFu;
-          load_tab(t.mtab, on ? (m & 0xFFFFu) : 65535u, T[i]);  // mtab[65535] = * 0
+          load_tab(t.mtab_tin, on ? (m & 0xFFFFu) : 65535u, T[i]);  // [65535] = * 0; tower out
           d[i] = make_uint2(0, 0);
           if (on) d[i] = wide ? *reinterpret_cast<const uint2 *>(colp + uint64_t(v) * sstride)
                               : load8_any(colp + uint64_t(v) * sstride, avail);
@@ -468,7 +496,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         for (int e = 0; e < 64; ++e)  // constant trip count: w stays in registers
           if (uint64_t(e) < avail) w[half][e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
       }
-      load_tab(t.mtab, meta[half] & 0xffffu, RT[half]);
+      load_tab(t.mtab_tin, meta[half] & 0xffffu, RT[half]);  // scaled into tower coordinates
     };
     if ((meta[0] & 0xffffu) != 0xffffu) load_row(0);
     STAMP(0);
@@ -515,8 +543,9 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t m = (meta[2 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
-      if constexpr (PACKED) load_tab(t.mtab, m != 0xFFFFu ? m : 0u, T5[q]);  // defined on every path
-      else if (m != 0xFFFFu) load_tab(t.mtab, m, T5[q]);
+      // tower coordinates in, symbols out
+      if constexpr (PACKED) load_tab(t.mtab_tout, m != 0xFFFFu ? m : 0u, T5[q]);  // defined on every path
+      else if (m != 0xFFFFu) load_tab(t.mtab_tout, m, T5[q]);
     }
 
     // ---- phase 2: IFFT_1024 on this wave's group
@@ -568,7 +597,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     // stage 9 is b ^= a only, stage 8 multiplies in its p9 = 1 block only.  The
     // p8 = p9 = 1 registers (4 hi + 3) are not needed past stage 8.
     {
-      Tab Tb;
+      SubTab Tb;
       tab_at(tabs, tlin(skew_idx(1u << 9, 8)), Tb);
 #pragma unroll
       for (int hi = 0; hi < 4; ++hi) {
@@ -634,8 +663,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     STAMP(7);
     {
       // q bit0 = p6, bit1 = p7; lane bits = p0..p5.  Positions < 256 only.
-      auto fb = [&](int a, int bb, const Tab &T) {
-        mul_acc(ql[bb], qh[bb], T, ql[a], qh[a]);
+      auto fb = [&](int a, int bb, const SubTab &T) {  // every stage >= SUB for y < 256
+        mul_acc_sub(ql[bb], qh[bb], T, ql[a], qh[a]);
         ql[bb] ^= ql[a];
         qh[bb] ^= qh[a];
       };
@@ -654,12 +683,14 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
           case 6: return tlin(skew_idx(hi47 | lo01, 3));
           case 7: return tlin(skew_idx(hi47 | lo01, 2));
           case 8: return tlin(skew_idx(hi47 | 8u | lo01, 2));
-          case 9: return tlin(skew_idx(hi27, 1));
-          case 10: return tlin(skew_idx(hi27, 0));
-          default: return tlin(skew_idx(hi27 | 2u, 0));
+          // stages 1, 0: their image slots hold general tables; the stage-2
+          // slot of the same (subfield) skew element instead (sub_alias)
+          case 9: return tlin(sub_alias(hi27, 1));
+          case 10: return tlin(sub_alias(hi27, 0));
+          default: return tlin(sub_alias(hi27 | 2u, 0));
         }
       };
-      Tab T[2];
+      SubTab T[2];
       tab_at(tabs, L(0), T[0]);
       tab_at(tabs, L(1), T[1]);
       fb(0, 2, T[0]);  // stage 7

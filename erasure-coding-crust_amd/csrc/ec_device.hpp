@@ -138,6 +138,46 @@ __device__ __forceinline__ void mul_acc(uint32_t xl, uint32_t xh, const Tab &T, 
   yh = h;
 }
 
+// ---- subfield multiplies in tower coordinates -------------
+// Symbols < 256 are the subfield GF(2^8).  In tower coordinates
+// (gf_field.hpp: x -> x ^ L(x >> 8), an involution) a multiply by a subfield
+// constant c acts on each byte alone, as GF(2^8) multiplication by c, so one
+// 8-bit table (3 + 3 + 2 bit groups: 5 dwords) serves both byte planes:
+// 6 v_perm + 6 v_and + 2 v_lshrrev_b64 + 4 XOR = 24 issue slots per 4
+// multiply-accumulates (mul_acc: 38).  SubTab words: t[0..1] group [0:3),
+// t[2..3] group [3:6), t[4] group [6:8) (MulTabSub, gf_field.hpp).
+struct SubTab {
+  uint32_t t[5];
+};
+
+__device__ __forceinline__ void mul_acc_sub(uint32_t xl, uint32_t xh, const SubTab &T, uint32_t &yl,
+                                            uint32_t &yh) {
+  const uint64_t x = (uint64_t(xh) << 32) | xl;
+  const uint64_t t3 = shr64<3>(x), t6 = shr64<6>(x);
+  const uint32_t s0 = xl & 0x07070707u;
+  const uint32_t s1 = uint32_t(t3) & 0x07070707u;
+  const uint32_t s2 = uint32_t(t6) & 0x03030303u;
+  const uint32_t s3 = xh & 0x07070707u;
+  const uint32_t s4 = uint32_t(t3 >> 32) & 0x07070707u;
+  const uint32_t s5 = uint32_t(t6 >> 32) & 0x03030303u;
+  yl = xor3(yl, vperm(T.t[1], T.t[0], s0), vperm(T.t[3], T.t[2], s1)) ^ vperm(T.t[4], T.t[4], s2);
+  yh = xor3(yh, vperm(T.t[1], T.t[0], s3), vperm(T.t[3], T.t[2], s4)) ^ vperm(T.t[4], T.t[4], s5);
+}
+
+// A subfield table in a tower LDS image (same slots as the general tables:
+// plane 0 holds t[0..3], the first dword of plane 1 holds t[4]) at absolute
+// LDS address `a` (plane 0).
+template <int PLANE>
+__device__ __forceinline__ void lds_subtab_abs(uint32_t a, SubTab &T) {
+  T.t[4] = *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t(a + PLANE));
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u v = *(const __attribute__((address_space(3))) v4u *)(uintptr_t(a));
+  T.t[0] = v.x;
+  T.t[1] = v.y;
+  T.t[2] = v.z;
+  T.t[3] = v.w;
+}
+
 // LDS-resident multiply tables: plane-major (5 planes of 16-byte chunks), the
 // 16-byte slot of entry idx XOR-swizzled by f(idx) = (idx ^ idx>>4 ^ idx>>8) & 15.
 // f is injective on every set of entries one ds_read_b128 lane group touches in

@@ -17,10 +17,20 @@ namespace ecamd {
 constexpr size_t kTabImageBytes = 5 * 1024 * 16;
 constexpr int kTabImages = 4;
 
+// Tower images: the same slots in tower coordinates.  Entry
+// i of set q is a subfield table (MulTabSub: plane 0 = w[0..3], dword 0 of
+// plane 1 = w[4]) when its stage ctz(1024 q + i + 1) >= tower_sub_min(q) --
+// every such skew is < 256 -- and a general tower table (Field::tower_tab)
+// below; a kernel reading set q uses mul_acc_sub at exactly those stages.
+constexpr int tower_sub_min(int q) { return q == 0 ? 2 : q == 1 ? 3 : 4; }
+
 struct DevTables {
-  const uint16_t *skews = nullptr;  // 65535
-  const MulTab *mtab = nullptr;     // 65536
-  const uint8_t *timg = nullptr;    // kTabImages x kTabImageBytes
+  const uint16_t *skews = nullptr;     // 65535
+  const MulTab *mtab = nullptr;        // 65536
+  const uint8_t *timg = nullptr;       // kTabImages x kTabImageBytes
+  const MulTab *mtab_tin = nullptr;    // 65536, symbols in, tower out
+  const MulTab *mtab_tout = nullptr;   // 65536, tower in, symbols out
+  const uint8_t *timg_t = nullptr;     // kTabImages x kTabImageBytes, tower images
 };
 
 // Per (device, kernel), once and thread-safe: raise `fn`'s dynamic-LDS limit

@@ -19,6 +19,8 @@ struct DeviceState {
   uint16_t *skews = nullptr;
   MulTab *mtab = nullptr;
   uint8_t *timg = nullptr;
+  MulTab *mtab_t = nullptr;  // mtab_tin, then mtab_tout
+  uint8_t *timg_t = nullptr;
   std::mutex mu;
   std::map<uint32_t, uint16_t *> fold;
   std::mutex scratch_mu;  // held by a ScratchLease
@@ -82,19 +84,40 @@ DeviceState *device_state() {
                         hipMemcpyHostToDevice),
               "upload mtab"))
     return nullptr;
-  // LDS table images (ec_kernels.hpp kTabImages): LdsTabs<1024>::addr layout
-  std::vector<uint8_t> img(kTabImages * kTabImageBytes, 0);
+  // LDS table images (ec_kernels.hpp kTabImages): LdsTabs<1024>::addr layout;
+  // img_t: the tower images (subfield tables at stages >= tower_sub_min(q))
+  std::vector<uint8_t> img(kTabImages * kTabImageBytes, 0), img_t(kTabImages * kTabImageBytes, 0);
   for (int q = 0; q < kTabImages; ++q)
     for (uint32_t i = 0; i < 1023; ++i) {
-      const uint8_t *src = reinterpret_cast<const uint8_t *>(&f.mtab[f.skews[1024 * q + i]]);
+      const uint32_t c = f.skews[1024 * q + i];
+      const uint8_t *src = reinterpret_cast<const uint8_t *>(&f.mtab[c]);
       const uint32_t sw = (i ^ (i >> 4) ^ (i >> 8)) & 15;
-      for (uint32_t plane = 0; plane < 5; ++plane)
-        std::memcpy(&img[q * kTabImageBytes + plane * 16384 + ((i >> 4) << 8) + (sw << 4)],
-                    src + 16 * plane, 16);
+      const size_t slot = size_t(q) * kTabImageBytes + ((i >> 4) << 8) + (sw << 4);
+      for (uint32_t plane = 0; plane < 5; ++plane) std::memcpy(&img[slot + plane * 16384], src + 16 * plane, 16);
+      if (__builtin_ctz(1024 * q + i + 1) >= tower_sub_min(q)) {
+        const MulTabSub u = f.sub_tab(c);
+        std::memcpy(&img_t[slot], &u.w[0], 16);
+        std::memcpy(&img_t[slot + 16384], &u.w[4], 4);
+      } else {
+        const MulTab g = f.tower_tab(c);
+        for (uint32_t plane = 0; plane < 5; ++plane)
+          std::memcpy(&img_t[slot + plane * 16384], reinterpret_cast<const uint8_t *>(&g) + 16 * plane, 16);
+      }
     }
   if (!hip_ok(hipMalloc(&st->timg, img.size()), "hipMalloc(table images)") ||
       !hip_ok(hipMemcpy(st->timg, img.data(), img.size(), hipMemcpyHostToDevice),
-              "upload table images"))
+              "upload table images") ||
+      !hip_ok(hipMalloc(&st->timg_t, img_t.size()), "hipMalloc(tower images)") ||
+      !hip_ok(hipMemcpy(st->timg_t, img_t.data(), img_t.size(), hipMemcpyHostToDevice),
+              "upload tower images"))
+    return nullptr;
+  if (!hip_ok(hipMalloc(&st->mtab_t, 2 * f.mtab.size() * sizeof(MulTab)), "hipMalloc(tower mtab)") ||
+      !hip_ok(hipMemcpy(st->mtab_t, f.mtab_tin.data(), f.mtab_tin.size() * sizeof(MulTab),
+                        hipMemcpyHostToDevice),
+              "upload mtab_tin") ||
+      !hip_ok(hipMemcpy(st->mtab_t + f.mtab.size(), f.mtab_tout.data(),
+                        f.mtab_tout.size() * sizeof(MulTab), hipMemcpyHostToDevice),
+              "upload mtab_tout"))
     return nullptr;
   // load the library's code object now (the first kernel launch of a process
   // loads it, ~1 ms): one one-lane launch, so no C-ABI call's timed region
@@ -113,6 +136,9 @@ DevTables device_tables(DeviceState *d) {
   t.skews = d->skews;
   t.mtab = d->mtab;
   t.timg = d->timg;
+  t.mtab_tin = d->mtab_t;
+  t.mtab_tout = d->mtab_t + kFieldSize;
+  t.timg_t = d->timg_t;
   return t;
 }
 

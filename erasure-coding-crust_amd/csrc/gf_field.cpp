@@ -67,37 +67,77 @@ void build_skews(Field &f) {  // additive_fft.hpp:47-97
   for (uint32_t i = 0; i < kOneMask; ++i) f.skews[i] = f.log[elem[i]];
 }
 
-// byte table of `cnt` entries: entry v = selected byte of (v << pos) * g^c
-uint32_t pack4(const Field &f, uint32_t c, bool zero, uint32_t pos, uint32_t first, bool high) {
+// byte table of 4 entries: entry e = selected byte of f((first + e) << pos)
+template <typename F>
+uint32_t pack4(F f, uint32_t pos, uint32_t first, bool high) {
   uint32_t w = 0;
   for (uint32_t e = 0; e < 4; ++e) {
-    const uint32_t v = first + e;
-    const uint16_t p = zero ? 0 : f.mul(uint16_t(v << pos), c);
+    const uint16_t p = f(uint16_t((first + e) << pos));
     w |= uint32_t(high ? (p >> 8) : (p & 0xff)) << (8 * e);
   }
   return w;
 }
 
+// v_perm table set (MulTab layout) of any GF(2)-linear map f on symbols
+template <typename F>
+MulTab make_tab(F f) {
+  MulTab t;
+  const uint32_t pos3[4] = {0, 3, 8, 11};
+  for (int g = 0; g < 4; ++g) {
+    t.w[4 * g + 0] = pack4(f, pos3[g], 0, false);
+    t.w[4 * g + 1] = pack4(f, pos3[g], 4, false);
+    t.w[4 * g + 2] = pack4(f, pos3[g], 0, true);
+    t.w[4 * g + 3] = pack4(f, pos3[g], 4, true);
+  }
+  t.w[16] = pack4(f, 6, 0, false);
+  t.w[17] = pack4(f, 6, 0, true);
+  t.w[18] = pack4(f, 14, 0, false);
+  t.w[19] = pack4(f, 14, 0, true);
+  return t;
+}
+
 void build_mtab(Field &f) {
+  // L(bit i of the high byte) = 2^(8+i) + 2^i * w, w = 0x100 (gf_field.hpp)
+  uint8_t lb[8];
+  for (uint32_t i = 0; i < 8; ++i) {
+    const uint32_t v = (1u << (8 + i)) ^ f.mul(uint16_t(1u << i), f.log[0x100]);
+    lb[i] = uint8_t(v);  // v < 256: the subfield part (checked by tests/cpp/tower_check.cpp)
+  }
+  for (uint32_t h = 0; h < 256; ++h) {
+    uint8_t l = 0;
+    for (uint32_t i = 0; i < 8; ++i)
+      if ((h >> i) & 1) l ^= lb[i];
+    f.tower_l[h] = l;
+  }
   f.mtab.resize(kFieldSize);
+  f.mtab_tin.resize(kFieldSize);
+  f.mtab_tout.resize(kFieldSize);
   for (uint32_t c = 0; c < kFieldSize; ++c) {
     const bool zero = (c == kZeroTab);
-    MulTab &t = f.mtab[c];
-    const uint32_t pos3[4] = {0, 3, 8, 11};
-    for (int g = 0; g < 4; ++g) {
-      t.w[4 * g + 0] = pack4(f, c, zero, pos3[g], 0, false);
-      t.w[4 * g + 1] = pack4(f, c, zero, pos3[g], 4, false);
-      t.w[4 * g + 2] = pack4(f, c, zero, pos3[g], 0, true);
-      t.w[4 * g + 3] = pack4(f, c, zero, pos3[g], 4, true);
-    }
-    t.w[16] = pack4(f, c, zero, 6, 0, false);
-    t.w[17] = pack4(f, c, zero, 6, 0, true);
-    t.w[18] = pack4(f, c, zero, 14, 0, false);
-    t.w[19] = pack4(f, c, zero, 14, 0, true);
+    const Field &cf = f;
+    f.mtab[c] = make_tab([&](uint16_t x) { return zero ? uint16_t(0) : cf.mul(x, c); });
+    f.mtab_tin[c] = make_tab([&](uint16_t x) { return zero ? uint16_t(0) : cf.tower(cf.mul(x, c)); });
+    f.mtab_tout[c] = make_tab([&](uint16_t x) { return zero ? uint16_t(0) : cf.mul(cf.tower(x), c); });
   }
 }
 
 }  // namespace
+
+MulTab Field::tower_tab(uint32_t c) const {
+  if (c == kZeroTab) return mtab[kZeroTab];
+  return make_tab([&](uint16_t x) { return tower(mul(tower(x), c)); });
+}
+
+MulTabSub Field::sub_tab(uint32_t c) const {
+  MulTabSub t;
+  const auto f = [&](uint16_t x) { return c == kZeroTab ? uint16_t(0) : mul(x, c); };  // < 256 for x < 256
+  t.w[0] = pack4(f, 0, 0, false);
+  t.w[1] = pack4(f, 0, 4, false);
+  t.w[2] = pack4(f, 3, 0, false);
+  t.w[3] = pack4(f, 3, 4, false);
+  t.w[4] = pack4(f, 6, 0, false);
+  return t;
+}
 
 std::vector<uint16_t> Field::fold_log_walsh(uint32_t n) const {
   std::vector<uint16_t> F(n);

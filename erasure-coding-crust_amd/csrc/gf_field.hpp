@@ -37,10 +37,34 @@ static_assert(sizeof(MulTab) == 80, "MulTab layout");
 // mean "no multiply" in additive_fft.hpp:110,129 == multiply by zero.
 constexpr uint32_t kZeroTab = 65535;
 
+// Tower coordinates.  The symbols < 256 are the subfield
+// GF(2^8) (closed under the reference's multiplication), and with w = 0x100
+// every symbol is x0 + x1 * w, x0, x1 < 256, where x1 = x >> 8 and
+// x0 = (x & 0xFF) ^ L(x >> 8) for the GF(2)-linear L below; the map
+// x -> x0 | x1 << 8 is therefore x ^ L(x >> 8), its own inverse.  A multiply by
+// a subfield constant c acts on tower coordinates bytewise: (c x0, c x1).
+// Addition (XOR) is the same in both coordinates, so an FFT runs unchanged in
+// tower coordinates as long as its multiply tables are conjugated by the map.
+//
+// Subfield table of a constant c (log domain, g^c < 256), 5 dwords: byte e of
+// w[0..1] = (e) * g^c, of w[2..3] = (e << 3) * g^c, of w[4] = (e << 6) * g^c.
+struct MulTabSub {
+  uint32_t w[5];
+};
+
 struct Field {
   std::vector<uint16_t> log, exp, log_walsh;  // 65536 each (f2e16.hpp:48-84)
   std::vector<uint16_t> skews;                // 65535 (additive_fft.hpp:47-97)
   std::vector<MulTab> mtab;                   // 65536: [c] = *g^c, [65535] = *0
+  // tower-coordinate variants (65536 each, [65535] = *0): x -> T(x * g^c)
+  // (symbols in, tower out) and x -> T(x) * g^c (tower in, symbols out)
+  std::vector<MulTab> mtab_tin, mtab_tout;
+  uint8_t tower_l[256];  // L on a high byte
+
+  uint16_t tower(uint16_t x) const { return uint16_t(x ^ tower_l[x >> 8]); }
+  // general table of x -> T(T(x) * g^c) (tower in and out)
+  MulTab tower_tab(uint32_t c) const;
+  MulTabSub sub_tab(uint32_t c) const;  // requires g^c < 256 (or c = 65535)
 
   uint16_t mul(uint16_t x, uint32_t log_c) const {
     if (x == 0) return 0;
