@@ -164,6 +164,35 @@ __device__ __forceinline__ void mul_acc_sub(uint32_t xl, uint32_t xh, const SubT
   yh = xor3(yh, vperm(T.t[1], T.t[0], s3), vperm(T.t[3], T.t[2], s4)) ^ vperm(T.t[4], T.t[4], s5);
 }
 
+// symbol <-> tower coordinates of a byte-planar group (the map is its own
+// inverse): l ^= L(h) bytewise, L = kTowerL, as compile-time v_perm tables
+__host__ __device__ constexpr uint8_t tower_l8(uint32_t h) {
+  uint8_t r = 0;
+  for (int i = 0; i < 8; ++i)
+    if ((h >> i) & 1) r ^= kTowerL[i];
+  return r;
+}
+__host__ __device__ constexpr uint32_t tower_word(uint32_t pos, uint32_t first) {
+  uint32_t w = 0;
+  for (uint32_t e = 0; e < 4; ++e) w |= uint32_t(tower_l8((first + e) << pos)) << (8 * e);
+  return w;
+}
+struct TowerK {  // the five table words in VGPRs
+  uint32_t w[5];
+};
+// materialised where the conversion runs (opaque: not hoisted out of a loop
+// and kept live across it)
+__device__ __forceinline__ TowerK tower_k() {
+  TowerK k = {{tower_word(0, 0), tower_word(0, 4), tower_word(3, 0), tower_word(3, 4), tower_word(6, 0)}};
+#pragma unroll
+  for (int i = 0; i < 5; ++i) asm volatile("" : "+v"(k.w[i]));
+  return k;
+}
+__device__ __forceinline__ uint32_t tower_lo(uint32_t l, uint32_t h, const TowerK &k) {
+  const uint32_t s0 = h & 0x07070707u, s1 = (h >> 3) & 0x07070707u, s2 = (h >> 6) & 0x03030303u;
+  return xor3(l, vperm(k.w[1], k.w[0], s0), vperm(k.w[3], k.w[2], s1)) ^ vperm(k.w[4], k.w[4], s2);
+}
+
 // A subfield table in a tower LDS image (same slots as the general tables:
 // plane 0 holds t[0..3], the first dword of plane 1 holds t[4]) at absolute
 // LDS address `a` (plane 0).

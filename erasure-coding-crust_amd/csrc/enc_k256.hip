@@ -19,6 +19,8 @@
 // include/ec-cpp/additive_fft.hpp:99-141 and poly_encoder.hpp:217-240.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "ec_device.hpp"
 #include "ec_kernels.hpp"
 
@@ -62,25 +64,56 @@ __device__ __forceinline__ void lds_tab_at(const uint8_t *lds, uint32_t lin, Tab
   }
 }
 
+// subfield table (tower image): plane 0 and dword 0 of plane 1
+__device__ __forceinline__ void lds_tab_at(const uint8_t *lds, uint32_t lin, SubTab &T) {
+  T.t[4] = *reinterpret_cast<const uint32_t *>(lds + Tabs::kPlane + lin);
+  const uint4 v = *reinterpret_cast<const uint4 *>(lds + lin);
+  T.t[0] = v.x;
+  T.t[1] = v.y;
+  T.t[2] = v.z;
+  T.t[3] = v.w;
+}
+// table type of stage m in a tower image whose subfield stages start at SM
+template <bool SUBF>
+struct TabSel {
+  using type = Tab;
+};
+template <>
+struct TabSel<true> {
+  using type = SubTab;
+};
+template <int M, int SM>
+using TabAt = typename TabSel<(M >= SM)>::type;
+
+__device__ __forceinline__ void mul_any(uint32_t xl, uint32_t xh, const Tab &T, uint32_t &yl, uint32_t &yh) {
+  mul_acc(xl, xh, T, yl, yh);
+}
+__device__ __forceinline__ void mul_any(uint32_t xl, uint32_t xh, const SubTab &T, uint32_t &yl,
+                                        uint32_t &yh) {
+  mul_acc_sub(xl, xh, T, yl, yh);
+}
+
 // skew index of the block holding position pos_a at stage m (additive_fft.hpp:108,126)
 __device__ __forceinline__ uint32_t skew_idx(uint32_t pos_a, int m, uint32_t offset) {
   const uint32_t d = 1u << m;
   return (pos_a & ~(2 * d - 1)) + d - 1 + offset;
 }
 
-__device__ __forceinline__ void ibfly(State &s, int ra, int rb, const Tab &T) {
+template <typename T>
+__device__ __forceinline__ void ibfly(State &s, int ra, int rb, const T &Tb) {
 #pragma unroll
   for (int g = 0; g < GP; ++g) {
     s.l[g][rb] ^= s.l[g][ra];
     s.h[g][rb] ^= s.h[g][ra];
-    mul_acc(s.l[g][rb], s.h[g][rb], T, s.l[g][ra], s.h[g][ra]);
+    mul_any(s.l[g][rb], s.h[g][rb], Tb, s.l[g][ra], s.h[g][ra]);
   }
 }
 
-__device__ __forceinline__ void fbfly(State &s, int ra, int rb, const Tab &T) {
+template <typename T>
+__device__ __forceinline__ void fbfly(State &s, int ra, int rb, const T &Tb) {
 #pragma unroll
   for (int g = 0; g < GP; ++g) {
-    mul_acc(s.l[g][rb], s.h[g][rb], T, s.l[g][ra], s.h[g][ra]);
+    mul_any(s.l[g][rb], s.h[g][rb], Tb, s.l[g][ra], s.h[g][ra]);
     s.l[g][rb] ^= s.l[g][ra];
     s.h[g][rb] ^= s.h[g][ra];
   }
@@ -91,60 +124,65 @@ __device__ __forceinline__ void fbfly(State &s, int ra, int rb, const Tab &T) {
 // table load in flight instead of stalling on each (2 x 20 VGPRs).
 // radix-8 pass over 3 consecutive position bits b0..b0+2 held in registers:
 // pos(r) = base | (r << b0).  Inverse: stages b0, b0+1, b0+2.
-__device__ __forceinline__ void ipass3(State &s, const uint8_t *tabs, uint32_t base, int b0,
-                                       uint32_t off) {
+// Stages >= SM (the tower image's subfield stages) multiply with SubTab.
+template <int b0, int SM>
+__device__ __forceinline__ void ipass3(State &s, const uint8_t *tabs, uint32_t base, uint32_t off) {
   {
-    Tab Ta, Tb;
+    TabAt<b0, SM> Ta0, Tb0;
+    TabAt<b0 + 1, SM> Ta1, Tb1;
+    TabAt<b0 + 2, SM> Ta2;
     const uint32_t lb = tlin(base & ~((2u << b0) - 1));  // lane part of every index below
     const auto i0 = [&](int rr) { return lb ^ tlin(skew_idx(uint32_t(2 * rr) << b0, b0, off)); };
     const auto i1 = [&](int hh) { return lb ^ tlin(skew_idx(uint32_t(4 * hh) << b0, b0 + 1, off)); };
     const uint32_t i2 = lb ^ tlin(skew_idx(0, b0 + 2, off));
-    lds_tab_at(tabs, i0(0), Ta);
-    lds_tab_at(tabs, i0(1), Tb);
-    ibfly(s, 0, 1, Ta);
-    lds_tab_at(tabs, i0(2), Ta);
-    ibfly(s, 2, 3, Tb);
-    lds_tab_at(tabs, i0(3), Tb);
-    ibfly(s, 4, 5, Ta);
-    lds_tab_at(tabs, i1(0), Ta);
-    ibfly(s, 6, 7, Tb);
-    lds_tab_at(tabs, i1(1), Tb);
-    ibfly(s, 0, 2, Ta);
-    ibfly(s, 1, 3, Ta);
-    lds_tab_at(tabs, i2, Ta);
-    ibfly(s, 4, 6, Tb);
-    ibfly(s, 5, 7, Tb);
+    lds_tab_at(tabs, i0(0), Ta0);
+    lds_tab_at(tabs, i0(1), Tb0);
+    ibfly(s, 0, 1, Ta0);
+    lds_tab_at(tabs, i0(2), Ta0);
+    ibfly(s, 2, 3, Tb0);
+    lds_tab_at(tabs, i0(3), Tb0);
+    ibfly(s, 4, 5, Ta0);
+    lds_tab_at(tabs, i1(0), Ta1);
+    ibfly(s, 6, 7, Tb0);
+    lds_tab_at(tabs, i1(1), Tb1);
+    ibfly(s, 0, 2, Ta1);
+    ibfly(s, 1, 3, Ta1);
+    lds_tab_at(tabs, i2, Ta2);
+    ibfly(s, 4, 6, Tb1);
+    ibfly(s, 5, 7, Tb1);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ibfly(s, r, r + 4, Ta);
+    for (int r = 0; r < 4; ++r) ibfly(s, r, r + 4, Ta2);
   }
 }
 
 // forward: stages b0+2, b0+1, b0
-__device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t base, int b0,
-                                       uint32_t off) {
+template <int b0, int SM>
+__device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t base, uint32_t off) {
   {
-    Tab Ta, Tb;
+    TabAt<b0, SM> Ta0, Tb0;
+    TabAt<b0 + 1, SM> Ta1, Tb1;
+    TabAt<b0 + 2, SM> Ta2;
     const uint32_t lb = tlin(base & ~((2u << b0) - 1));  // lane part of every index below
     const auto i0 = [&](int rr) { return lb ^ tlin(skew_idx(uint32_t(2 * rr) << b0, b0, off)); };
     const auto i1 = [&](int hh) { return lb ^ tlin(skew_idx(uint32_t(4 * hh) << b0, b0 + 1, off)); };
     const uint32_t i2 = lb ^ tlin(skew_idx(0, b0 + 2, off));
-    lds_tab_at(tabs, i2, Ta);
-    lds_tab_at(tabs, i1(0), Tb);
+    lds_tab_at(tabs, i2, Ta2);
+    lds_tab_at(tabs, i1(0), Tb1);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) fbfly(s, r, r + 4, Ta);
-    lds_tab_at(tabs, i1(1), Ta);
-    fbfly(s, 0, 2, Tb);
-    fbfly(s, 1, 3, Tb);
-    lds_tab_at(tabs, i0(0), Tb);
-    fbfly(s, 4, 6, Ta);
-    fbfly(s, 5, 7, Ta);
-    lds_tab_at(tabs, i0(1), Ta);
-    fbfly(s, 0, 1, Tb);
-    lds_tab_at(tabs, i0(2), Tb);
-    fbfly(s, 2, 3, Ta);
-    lds_tab_at(tabs, i0(3), Ta);
-    fbfly(s, 4, 5, Tb);
-    fbfly(s, 6, 7, Ta);
+    for (int r = 0; r < 4; ++r) fbfly(s, r, r + 4, Ta2);
+    lds_tab_at(tabs, i1(1), Ta1);
+    fbfly(s, 0, 2, Tb1);
+    fbfly(s, 1, 3, Tb1);
+    lds_tab_at(tabs, i0(0), Tb0);
+    fbfly(s, 4, 6, Ta1);
+    fbfly(s, 5, 7, Ta1);
+    lds_tab_at(tabs, i0(1), Ta0);
+    fbfly(s, 0, 1, Tb0);
+    lds_tab_at(tabs, i0(2), Tb0);
+    fbfly(s, 2, 3, Ta0);
+    lds_tab_at(tabs, i0(3), Ta0);
+    fbfly(s, 4, 5, Tb0);
+    fbfly(s, 6, 7, Ta0);
   }
 }
 
@@ -162,7 +200,7 @@ __device__ __forceinline__ void bxor(State &s, int ra, int rb) {  // b ^= a (no 
 // the multiply): stage 7 (j = 128) and stage 6's first block (j = 64) are
 // b ^= a only.
 __device__ __forceinline__ void ipassC0(State &s, const uint8_t *tabs) {
-  Tab Tb;
+  SubTab Tb;  // stage 6 >= tower_sub_min(0)
   lds_tab_at(tabs, tlin(skew_idx(1u << 7, 6, 0)), Tb);
   bxor(s, 0, 1);  // stage 6, j = 64
   bxor(s, 4, 5);
@@ -175,7 +213,7 @@ __device__ __forceinline__ void ipassC0(State &s, const uint8_t *tabs) {
 }
 
 __device__ __forceinline__ void fpassC(State &s, const uint8_t *tabs, uint32_t off) {
-  Tab Ta, Tb;
+  SubTab Ta, Tb;  // stages 7, 6 >= tower_sub_min(0), tower_sub_min(1)
   lds_tab_at(tabs, tlin(skew_idx(0, 7, off)), Ta);
   lds_tab_at(tabs, tlin(skew_idx(0, 6, off)), Tb);
   fbfly(s, 0, 2, Ta);
@@ -417,12 +455,13 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
   // multiply tables for skew indices 0..1022: the prebuilt LDS image 0
   // (DevTables::timg), one coalesced 80 KB copy instead of a 1023-entry gather
   // through the skews (that gather was ~10 us of every launch; small calls pay it)
-  Tabs::copy_image<THREADS>(tabs, t.timg, tid0);
+  // the tower images: the transforms run in tower coordinates
+  Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);
   __syncthreads();
   [[maybe_unused]] int img = 0;
   [[maybe_unused]] const auto load_image = [&](int q) {  // LDS-DMA: no VGPRs (the kernel is at 128)
     lds_barrier();  // every wave is done with the current tables
-    Tabs::dma_image<THREADS>(tabs, t.timg + q * kTabImageBytes, tid0);
+    Tabs::dma_image<THREADS>(tabs, t.timg_t + q * kTabImageBytes, tid0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
   };
@@ -535,6 +574,11 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     rsync();
     store(0);
     __builtin_amdgcn_sched_barrier(0);
+    {  // into tower coordinates
+      const TowerK tk = tower_k();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) s.l[0][r] = tower_lo(s.l[0][r], s.h[0][r], tk);
+    }
 
     // ---- IFFT_256 (index 0): passes A (bits 0-2), B (3-5), C (6-7)
     if constexpr (N > 1024) {
@@ -543,16 +587,18 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
         img = 0;
       }
     }
-    ipass3(s, tabs, posA(q, 0), 0, 0);
+    ipass3<0, tower_sub_min(0)>(s, tabs, posA(q, 0), 0);
     rsync();  // systematic rows read out of the regions
     exchange<LA, LB>(s, xch, xb);
-    ipass3(s, tabs, posB(q, 0), 3, 0);
+    ipass3<3, tower_sub_min(0)>(s, tabs, posB(q, 0), 0);
     exchange<LB, LC>(s, xch, xb);
     ipassC0(s, tabs);
     const State coef = s;
 
     // ---- FFT_256 at each coset shift (encodeLow, poly_encoder.hpp:229-237)
-    const auto coset = [&](const uint32_t sh, const uint32_t off) __attribute__((always_inline)) {
+    // sm: the tower image's first subfield stage (std::integral_constant)
+    const auto coset = [&](auto sm, const uint32_t sh, const uint32_t off) __attribute__((always_inline)) {
+      constexpr int SM = decltype(sm)::value;
       s = coef;
       // opaque copy: keeps the compiler from hoisting the first stage's selector
       // masks out of the coset loop (that costs ~50 VGPRs and forces spills)
@@ -563,23 +609,29 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
       fpassC(s, tabs, off);
       rsync();  // previous coset's rows read out
       exchange<LC, LB>(s, xch, xb);
-      fpass3(s, tabs, posB(q, 0), 3, off);
+      fpass3<3, SM>(s, tabs, posB(q, 0), off);
       exchange<LB, LA>(s, xch, xb);
-      fpass3(s, tabs, posA(q, 0), 0, off);
+      fpass3<0, SM>(s, tabs, posA(q, 0), off);
+      {  // back to symbol coordinates
+        const TowerK tk = tower_k();
+#pragma unroll
+        for (int r = 0; r < 8; ++r) s.l[0][r] = tower_lo(s.l[0][r], s.h[0][r], tk);
+      }
       stage_own(s, xch, q, inst, wave);
       rsync();
       store(sh);
       __builtin_amdgcn_sched_barrier(0);
     };
-    if constexpr (N == 1024) {
-      for (uint32_t sh = K; sh < 1024u && int(sh) < nv; sh += K) coset(sh, sh);
-    } else {
-      for (uint32_t sh = K; sh < uint32_t(N) && int(sh) < nv; sh += K) {
+    using Sub0 = std::integral_constant<int, tower_sub_min(0)>;
+    using Sub1 = std::integral_constant<int, tower_sub_min(1)>;
+    for (uint32_t sh = K; sh < 1024u && int(sh) < nv; sh += K) coset(Sub0(), sh, sh);
+    if constexpr (N > 1024) {
+      for (uint32_t sh = 1024u; sh < uint32_t(N) && int(sh) < nv; sh += K) {
         if (sh == 1024u) {
           load_image(1);
           img = 1;
         }
-        coset(sh, sh & 1023u);
+        coset(Sub1(), sh, sh & 1023u);
       }
     }
   }

@@ -48,6 +48,11 @@ constexpr uint32_t kZeroTab = 65535;
 //
 // Subfield table of a constant c (log domain, g^c < 256), 5 dwords: byte e of
 // w[0..1] = (e) * g^c, of w[2..3] = (e << 3) * g^c, of w[4] = (e << 6) * g^c.
+// L on bit i of the high byte (w = 0x100): the device conversion
+// (ec_device.hpp tower_lo) is compiled from these; build_mtab derives L from
+// the field and tests/cpp/tower_check.cpp checks that the two agree
+constexpr uint8_t kTowerL[8] = {0x00, 0xcf, 0xab, 0x21, 0x8a, 0x9d, 0x27, 0x1f};
+
 struct MulTabSub {
   uint32_t w[5];
 };

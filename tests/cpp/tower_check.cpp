@@ -66,6 +66,8 @@ static uint16_t apply(M m, const T &tab, uint16_t x) {
 int main() {
   const Field &f = field();
   std::mt19937_64 rng(7);
+  // the device constants of L equal the field's
+  for (uint32_t i = 0; i < 8; ++i) CHECK(f.tower_l[1u << i] == kTowerL[i], "L bit %u", i);
   // the map is an involution, and the subfield is closed
   for (uint32_t x = 0; x < kFieldSize; ++x) CHECK(f.tower(f.tower(uint16_t(x))) == x, "x=%u", x);
   for (uint32_t a = 1; a < 256; a += 7)
