@@ -22,6 +22,8 @@
 // stays for the FFT) and finally replaced by the output tables E[y], y < k.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "ec_kernels.hpp"
 #include "tf1024.hpp"
 
@@ -38,8 +40,12 @@ static_assert(LDS_BYTES <= 160 * 1024 && Tabs::kBytes == kTabImageBytes, "LDS bu
 __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ? 0u : c; }
 
 // multiplier logs (65535 = multiply by zero) of the linearised cross-quarter part
+// The data runs in tower coordinates; every p_q / k_q is a
+// subfield element (skews 1023 / 2047 / 3071 are 0, 0 and 2: p, k in {0, 1, 2, 3}),
+// multiplied with its subfield table ps / ks.
 struct Lin {
   uint32_t p[4], k[4];
+  uint32_t ps[4][5], ks[4][5];
 };
 
 // Fold IFFT stages 10 (skews 1023 / 3071) and 11 (2047), the quarter bits of
@@ -72,6 +78,13 @@ Lin n4096_lin(int nq) {
     }
     lin.p[q] = P ? f.log[P] : 65535u;
     lin.k[q] = Q ? f.log[Q] : 65535u;
+    // subfield elements (tests/cpp/tower_check.cpp checks the skews' elements)
+    const MulTabSub sp = f.sub_tab(P < 256 ? lin.p[q] : 65535u), sk = f.sub_tab(Q < 256 ? lin.k[q] : 65535u);
+    for (int i = 0; i < 5; ++i) {
+      lin.ps[q][i] = sp.w[i];
+      lin.ks[q][i] = sk.w[i];
+    }
+    if (P >= 256 || Q >= 256) lin.p[0] = 0xDEAD;  // never: launch refuses (n4096_lin_ok)
   }
   return lin;
 }
@@ -164,9 +177,11 @@ reconstruct_n4096(
       } else {
         load_row_tail64(row, avail, w);
       }
-      load_tab(t.mtab, mq[half] & 0xffffu, RT);
+      load_tab(t.mtab_tin, mq[half] & 0xffffu, RT);  // scaled into tower coordinates
     };
-    const auto quarter = [&](const int q, const int qnext) __attribute__((always_inline)) {
+    // qc: std::integral_constant quarter (its tower image's subfield stages)
+    const auto quarter = [&](auto qc, const int qnext) __attribute__((always_inline)) {
+      constexpr int q = decltype(qc)::value;
       S16 Qq;
       __builtin_amdgcn_sched_barrier(0);
       uint32_t tq = tid;
@@ -212,13 +227,13 @@ reconstruct_n4096(
       // priority from quarter to quarter (as reconstruct_n1024's passes)
       if (((wave >> 2) ^ uint32_t(q)) & 1) __builtin_amdgcn_s_setprio(2);
       else __builtin_amdgcn_s_setprio(0);
-      if (q == 0) ifft1024<true>(Qq, tabs, my, lq);  // -> layout C; quarter 0 is at index 0
-      else ifft1024<false>(Qq, tabs, my, lq);
+      // -> layout C; quarter 0 is at index 0
+      ifft1024<q == 0, tower_sub_min(q)>(Qq, tabs, my, lq);
       __builtin_amdgcn_sched_barrier(0);
       if (qnext >= 0) {  // the next quarter's first row and tables
         if (has(0)) load_row(qnext, 0, w0, RT0);
         lds_barrier();  // every wave is done with this quarter's tables and its region
-        Tabs::dma_image<THREADS>(tabs, t.timg + qnext * kTabImageBytes, tq);
+        Tabs::dma_image<THREADS>(tabs, t.timg_t + qnext * kTabImageBytes, tq);
         __builtin_amdgcn_sched_barrier(0);
       }
       // P += p_q u_q, Qa += k_q u_q.  The constants are mostly 0 or 1 (the
@@ -237,11 +252,12 @@ reconstruct_n4096(
           P.h[r] ^= Qq.h[r];
         }
       } else if (ip != 65535u) {
-        Tab TP;
-        load_tab(t.mtab, ip, TP);
+        SubTab TP;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) TP.t[i] = lin.ps[q][i];
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          if (KB >= 9 || (r & 3) != 3) mul_acc(Qq.l[r], Qq.h[r], TP, P.l[r], P.h[r]);
+          if (KB >= 9 || (r & 3) != 3) mul_acc_sub(Qq.l[r], Qq.h[r], TP, P.l[r], P.h[r]);
       }
       if (ik == 0) {
 #pragma unroll
@@ -251,11 +267,12 @@ reconstruct_n4096(
             Qa.h[r] ^= Qq.h[r];
           }
       } else if (ik != 65535u) {
-        Tab TK;
-        load_tab(t.mtab, ik, TK);
+        SubTab TK;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) TK.t[i] = lin.ks[q][i];
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          if (live_above<LC, 10, KB>(r, KB - 1)) mul_acc(Qq.l[r], Qq.h[r], TK, Qa.l[r], Qa.h[r]);
+          if (live_above<LC, 10, KB>(r, KB - 1)) mul_acc_sub(Qq.l[r], Qq.h[r], TK, Qa.l[r], Qa.h[r]);
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r)  // accumulated here, not sunk into the next quarter's gather
@@ -270,13 +287,13 @@ reconstruct_n4096(
     load_meta(qfirst, tid);
     if (has(0)) load_row(qfirst, 0, w0, RT0);
     lds_barrier();  // every wave is done with the last tile's output tables and its region
-    Tabs::dma_image<THREADS>(tabs, t.timg + qfirst * kTabImageBytes, tid);
+    Tabs::dma_image<THREADS>(tabs, t.timg_t + qfirst * kTabImageBytes, tid);
     if constexpr (NQ == 4) {
-      if (3 * 1024 < nv) quarter(3, 2);
-      quarter(2, 1);
+      if (3 * 1024 < nv) quarter(std::integral_constant<int, 3>(), 2);
+      quarter(std::integral_constant<int, 2>(), 1);
     }
-    quarter(1, 0);
-    quarter(0, -1);
+    quarter(std::integral_constant<int, 1>(), 0);
+    quarter(std::integral_constant<int, 0>(), -1);
 
     // ---- cross-quarter IFFT stages (10, 11), the quarter bits of the formal
     // derivative and FFT stages 11 / 10 on the side that reaches y < 1024 are
@@ -298,8 +315,8 @@ reconstruct_n4096(
     // ---- FFT_1024, index 0 (quarter 0's tables still resident): whole for
     // k = 1024 (-> layout A: y = 16 lane + r), else restricted to y < k
     // (tf1024.hpp fft_restricted: live register pairs hold y0, y0 + 1)
-    if constexpr (KB == 10) fft1024<true>(Y, tabs, my, lane);
-    else fft_restricted<LC, 10, KB>(Y, tabs, lane);
+    if constexpr (KB == 10) fft1024<true, tower_sub_min(0)>(Y, tabs, my, lane);
+    else fft_restricted<LC, 10, KB, tower_sub_min(0)>(Y, tabs, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(Y.l[r]), "+v"(Y.h[r]));  // not sunk past the table gather
 
@@ -314,7 +331,7 @@ reconstruct_n4096(
       __builtin_amdgcn_sched_barrier(0);
     } else  // k = 256 / 512: the erased y < k only (nv = 2500 3.32 -> 3.20 ms per 512 x 1 MB)
       Tabs::gather_if<THREADS>(
-          tabs, t.mtab, [&](uint32_t y) { return mul_index(E[y]); },
+          tabs, t.mtab_tout, [&](uint32_t y) { return mul_index(E[y]); },  // tower in, symbols out
           [&](uint32_t y) { return y < K; }, [&](uint32_t y) { return !(int(y) < nv && pr[y]); }, tid);
     lds_barrier();
     if constexpr (KB < 10) {
@@ -435,10 +452,11 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
   uint8_t *oimg = static_cast<uint8_t *>(scratch) + gather_order_bytes(p, batch);
   if (p.k == 1024)
     hipLaunchKernelGGL(n4096_out_image, dim3(unsigned(batch)), dim3(256), 0, s, d_err_log, d_pattern,
-                       int(p.n), t.mtab, oimg);
+                       int(p.n), t.mtab_tout, oimg);  // tower in, symbols out
   const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   static const Lin lin4 = n4096_lin(4), lin2 = n4096_lin(2);
+  if (lin4.p[0] == 0xDEAD || lin2.p[0] == 0xDEAD) return hipErrorInvalidValue;  // not subfield (never)
 #define ECAMD_D4(NQv, KBv)                                                                    \
   if (p.n == 1024u * NQv && p.k == (1u << KBv))                                                  \
     hipLaunchKernelGGL((reconstruct_n4096<NQv, KBv>), dim3(grid), dim3(THREADS), LDS_BYTES, s,   \

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "ec_kernels.hpp"
 #include "tf1024.hpp"
@@ -114,6 +115,16 @@ __device__ __forceinline__ void load_group(S16 &s, const uint8_t *P, uint64_t pl
   }
 }
 
+// symbol <-> tower coordinates of both groups (an involution)
+__device__ __forceinline__ void to_tower(S16 &g0, S16 &g1) {
+  const TowerK tk = tower_k();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    g0.l[r] = tower_lo(g0.l[r], g0.h[r], tk);
+    g1.l[r] = tower_lo(g1.l[r], g1.h[r], tk);
+  }
+}
+
 // workgroup wg's coefficient slot, wave w, group g: 16 registers x 64 lanes
 __device__ __forceinline__ uint2 *coef_at(uint2 *scratch, uint64_t wg, uint32_t wave, int g) {
   return scratch + ((wg * WAVES + wave) * 2 + uint64_t(g)) * (16 * 64);
@@ -140,7 +151,8 @@ __global__ void __launch_bounds__(THREADS)
   const uint32_t ncos = uint32_t(nv + K - 1) / K;
   uint2 *const cw0 = coef_at(coef, blockIdx.x, wave, 0), *const cw1 = coef_at(coef, blockIdx.x, wave, 1);
 
-  Tabs::copy_image<THREADS>(tabs, t.timg, tid0);  // index 0 (the IFFT)
+  // tower images: the transforms run in tower coordinates
+  Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);  // index 0 (the IFFT)
   __syncthreads();
 
   const uint64_t npieces = slen / 2;
@@ -182,34 +194,38 @@ __global__ void __launch_bounds__(THREADS)
     // the index-0 tables (the last tile's DMA) landed; the regions are free
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
-    ifft1024<true>(g0, tabs, my, lane);
-    ifft1024<true>(g1, tabs, my, lane);
+    to_tower(g0, g1);
+    ifft1024<true, tower_sub_min(0)>(g0, tabs, my, lane);
+    ifft1024<true, tower_sub_min(0)>(g1, tabs, my, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {  // read back by cosets 2 and 3 (coset 1 uses the registers)
       cw0[r * 64 + lane] = make_uint2(g0.l[r], g0.h[r]);
       cw1[r * 64 + lane] = make_uint2(g1.l[r], g1.h[r]);
     }
     lds_barrier();  // every wave is done with the index-0 tables
-    Tabs::dma_image<THREADS>(tabs, t.timg + kTabImageBytes, tid);
-    const auto coset = [&](const uint32_t s) __attribute__((always_inline)) {
+    Tabs::dma_image<THREADS>(tabs, t.timg_t + kTabImageBytes, tid);
+    // cs: std::integral_constant coset number (its image's subfield stages)
+    const auto coset = [&](auto cs) __attribute__((always_inline)) {
+      constexpr uint32_t s = decltype(cs)::value;
       if (s > 1) load_coef();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // coset s's tables and coefficients landed
       lds_barrier();  // (all waves' slices) and the regions are free
-      fft1024(g0, tabs, my, lane);
-      fft1024(g1, tabs, my, lane);
+      fft1024<false, tower_sub_min(int(s))>(g0, tabs, my, lane);
+      fft1024<false, tower_sub_min(int(s))>(g1, tabs, my, lane);
+      to_tower(g0, g1);  // back to symbol coordinates
 #pragma unroll
       for (uint32_t hf = 0; hf < 2; ++hf) {
         if (hf) lds_barrier();
         stage_half(g0, g1, my, lane, wave, hf);
         lds_barrier();
         if (hf == 0)  // every wave is past its FFT: the next set (index 0 after the last coset)
-          Tabs::dma_image<THREADS>(tabs, t.timg + (s + 1 < ncos ? s + 1 : 0) * kTabImageBytes, tid);
+          Tabs::dma_image<THREADS>(tabs, t.timg_t + (s + 1 < ncos ? s + 1 : 0) * kTabImageBytes, tid);
         store_half(regions, SH, sstride, s * K + 512 * hf, nv, piece0, npieces, wave, lane);
       }
     };
-    coset(1);
-    coset(2);
-    if (ncos > 3) coset(3);
+    coset(std::integral_constant<uint32_t, 1>());
+    coset(std::integral_constant<uint32_t, 2>());
+    if (ncos > 3) coset(std::integral_constant<uint32_t, 3>());
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
 }

@@ -47,6 +47,28 @@ __device__ __forceinline__ void tab_at(const uint8_t *lds, uint32_t lin, Tab &T)
   }
 }
 
+// tower images: stages >= SM hold subfield tables; SM =
+// kNoTower: a symbol-coordinate image (every stage general)
+constexpr int kNoTower = 64;
+__device__ __forceinline__ void tab_at(const uint8_t *lds, uint32_t lin, SubTab &T) {
+  T.t[4] = *reinterpret_cast<const uint32_t *>(lds + Tabs::kPlane + lin);
+  const uint4 v = *reinterpret_cast<const uint4 *>(lds + lin);
+  T.t[0] = v.x;
+  T.t[1] = v.y;
+  T.t[2] = v.z;
+  T.t[3] = v.w;
+}
+template <bool SUBF>
+struct TabSel {
+  using type = Tab;
+};
+template <>
+struct TabSel<true> {
+  using type = SubTab;
+};
+template <int M, int SM>
+using TabAt = typename TabSel<(M >= SM)>::type;
+
 __device__ __forceinline__ uint32_t skew_idx(uint32_t pos_a, int m) {
   const uint32_t d = 1u << m;
   return (pos_a & ~(2 * d - 1)) + d - 1;
@@ -63,14 +85,30 @@ __device__ __forceinline__ void fb(S16 &s, int a, int b, const Tab &T) {  // for
   s.l[b] ^= s.l[a];
   s.h[b] ^= s.h[a];
 }
+__device__ __forceinline__ void ib(S16 &s, int a, int b, const SubTab &T) {
+  s.l[b] ^= s.l[a];
+  s.h[b] ^= s.h[a];
+  mul_acc_sub(s.l[b], s.h[b], T, s.l[a], s.h[a]);
+}
+__device__ __forceinline__ void fb(S16 &s, int a, int b, const SubTab &T) {
+  mul_acc_sub(s.l[b], s.h[b], T, s.l[a], s.h[a]);
+  s.l[b] ^= s.l[a];
+  s.h[b] ^= s.h[a];
+}
 
 // radix-16 passes over position bits B0..B0+3 held in registers; lb = tlin of
 // the lane part of the position.  The next block's table is requested one
 // step ahead of its use.
-template <int B0>
+template <int B0, int SM = kNoTower>
 __device__ __forceinline__ void ipass4(S16 &s, const uint8_t *tabs, uint32_t lb) {
   Tab T[2];
-  tab_at(tabs, lb ^ tlin(skew_idx(0, B0)), T[0]);
+  SubTab U[2];
+  const auto fetch = [&](int t, int blk, int slot) __attribute__((always_inline)) {
+    const uint32_t a = lb ^ tlin(skew_idx(uint32_t(blk) << B0, B0 + t));
+    if (B0 + t >= SM) tab_at(tabs, a, U[slot]);
+    else tab_at(tabs, a, T[slot]);
+  };
+  fetch(0, 0, 0);
   int k = 0;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -78,17 +116,26 @@ __device__ __forceinline__ void ipass4(S16 &s, const uint8_t *tabs, uint32_t lb)
 #pragma unroll
     for (int blk = 0; blk < 16; blk += 2 * d, ++k) {
       const int nt = blk + 2 * d < 16 ? t : t + 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
-      if (nt < 4) tab_at(tabs, lb ^ tlin(skew_idx(uint32_t(nblk) << B0, B0 + nt)), T[(k + 1) & 1]);
+      if (nt < 4) fetch(nt, nblk, (k + 1) & 1);
 #pragma unroll
-      for (int i = 0; i < d; ++i) ib(s, blk + i, blk + i + d, T[k & 1]);
+      for (int i = 0; i < d; ++i) {
+        if (B0 + t >= SM) ib(s, blk + i, blk + i + d, U[k & 1]);
+        else ib(s, blk + i, blk + i + d, T[k & 1]);
+      }
     }
   }
 }
 
-template <int B0>
+template <int B0, int SM = kNoTower>
 __device__ __forceinline__ void fpass4(S16 &s, const uint8_t *tabs, uint32_t lb) {
   Tab T[2];
-  tab_at(tabs, lb ^ tlin(skew_idx(0, B0 + 3)), T[0]);
+  SubTab U[2];
+  const auto fetch = [&](int t, int blk, int slot) __attribute__((always_inline)) {
+    const uint32_t a = lb ^ tlin(skew_idx(uint32_t(blk) << B0, B0 + t));
+    if (B0 + t >= SM) tab_at(tabs, a, U[slot]);
+    else tab_at(tabs, a, T[slot]);
+  };
+  fetch(3, 0, 0);
   int k = 0;
 #pragma unroll
   for (int t = 3; t >= 0; --t) {
@@ -96,32 +143,39 @@ __device__ __forceinline__ void fpass4(S16 &s, const uint8_t *tabs, uint32_t lb)
 #pragma unroll
     for (int blk = 0; blk < 16; blk += 2 * d, ++k) {
       const int nt = blk + 2 * d < 16 ? t : t - 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
-      if (nt >= 0) tab_at(tabs, lb ^ tlin(skew_idx(uint32_t(nblk) << B0, B0 + nt)), T[(k + 1) & 1]);
+      if (nt >= 0) fetch(nt, nblk, (k + 1) & 1);
 #pragma unroll
-      for (int i = 0; i < d; ++i) fb(s, blk + i, blk + i + d, T[k & 1]);
+      for (int i = 0; i < d; ++i) {
+        if (B0 + t >= SM) fb(s, blk + i, blk + i + d, U[k & 1]);
+        else fb(s, blk + i, blk + i + d, T[k & 1]);
+      }
     }
   }
 }
 
 // layout C: stage 8 (skew depends on p9 = r bit 1), stage 9 (one skew)
+template <int SM = kNoTower>
 __device__ __forceinline__ void ipassC(S16 &s, const uint8_t *tabs) {
-  Tab Ta, Tb;
+  TabAt<8, SM> Ta, Tb;
+  TabAt<9, SM> Tc;
   tab_at(tabs, tlin(skew_idx(0, 8)), Ta);
   tab_at(tabs, tlin(skew_idx(1u << 9, 8)), Tb);
 #pragma unroll
   for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi, 4 * hi + 1, Ta);
-  tab_at(tabs, tlin(skew_idx(0, 9)), Ta);
+  tab_at(tabs, tlin(skew_idx(0, 9)), Tc);
 #pragma unroll
   for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi + 2, 4 * hi + 3, Tb);
 #pragma unroll
   for (int hi = 0; hi < 4; ++hi) {
-    ib(s, 4 * hi, 4 * hi + 2, Ta);
-    ib(s, 4 * hi + 1, 4 * hi + 3, Ta);
+    ib(s, 4 * hi, 4 * hi + 2, Tc);
+    ib(s, 4 * hi + 1, 4 * hi + 3, Tc);
   }
 }
 
+template <int SM = kNoTower>
 __device__ __forceinline__ void fpassC(S16 &s, const uint8_t *tabs) {
-  Tab Ta, Tb;
+  TabAt<9, SM> Ta;
+  TabAt<8, SM> Tb, Tc;
   tab_at(tabs, tlin(skew_idx(0, 9)), Ta);
   tab_at(tabs, tlin(skew_idx(0, 8)), Tb);
 #pragma unroll
@@ -129,11 +183,11 @@ __device__ __forceinline__ void fpassC(S16 &s, const uint8_t *tabs) {
     fb(s, 4 * hi, 4 * hi + 2, Ta);
     fb(s, 4 * hi + 1, 4 * hi + 3, Ta);
   }
-  tab_at(tabs, tlin(skew_idx(1u << 9, 8)), Ta);
+  tab_at(tabs, tlin(skew_idx(1u << 9, 8)), Tc);
 #pragma unroll
   for (int hi = 0; hi < 4; ++hi) fb(s, 4 * hi, 4 * hi + 1, Tb);
 #pragma unroll
-  for (int hi = 0; hi < 4; ++hi) fb(s, 4 * hi + 2, 4 * hi + 3, Ta);
+  for (int hi = 0; hi < 4; ++hi) fb(s, 4 * hi + 2, 4 * hi + 3, Tc);
 }
 
 // The same two passes for the transform at index 0, where a stage's block at
@@ -145,8 +199,9 @@ __device__ __forceinline__ void bx(S16 &s, int a, int b) {  // b ^= a
   s.h[b] ^= s.h[a];
 }
 
+template <int SM = kNoTower>
 __device__ __forceinline__ void ipassC0(S16 &s, const uint8_t *tabs) {
-  Tab Tb;
+  TabAt<8, SM> Tb;
   tab_at(tabs, tlin(skew_idx(1u << 9, 8)), Tb);
 #pragma unroll
   for (int hi = 0; hi < 4; ++hi) bx(s, 4 * hi, 4 * hi + 1);
@@ -159,8 +214,9 @@ __device__ __forceinline__ void ipassC0(S16 &s, const uint8_t *tabs) {
   }
 }
 
+template <int SM = kNoTower>
 __device__ __forceinline__ void fpassC0(S16 &s, const uint8_t *tabs) {
-  Tab Ta;
+  TabAt<8, SM> Ta;
   tab_at(tabs, tlin(skew_idx(1u << 9, 8)), Ta);
 #pragma unroll
   for (int hi = 0; hi < 4; ++hi) {
@@ -224,27 +280,28 @@ __device__ __forceinline__ void exchange(S16 &s, uint8_t *my, uint32_t lane) {
 
 // IFFT_1024 (inverse_afft, index = the tables' offset; INDEX0: the offset is
 // 0): layout A in, C out
-template <bool INDEX0 = false>
+// SM: the table image's first subfield stage (tower images; kNoTower: none)
+template <bool INDEX0 = false, int SM = kNoTower>
 __device__ __forceinline__ void ifft1024(S16 &s, const uint8_t *tabs, uint8_t *my, uint32_t lane) {
   asm volatile("" : "+v"(lane));
-  ipass4<0>(s, tabs, tlin(16 * lane));
+  ipass4<0, SM>(s, tabs, tlin(16 * lane));
   exchange<LA, LB>(s, my, lane);
-  ipass4<4>(s, tabs, tlin((lane >> 4) << 8));
+  ipass4<4, SM>(s, tabs, tlin((lane >> 4) << 8));
   exchange<LB, LC>(s, my, lane);
-  if constexpr (INDEX0) ipassC0(s, tabs);
-  else ipassC(s, tabs);
+  if constexpr (INDEX0) ipassC0<SM>(s, tabs);
+  else ipassC<SM>(s, tabs);
 }
 
 // FFT_1024 (afft): layout C in, A out
-template <bool INDEX0 = false>
+template <bool INDEX0 = false, int SM = kNoTower>
 __device__ __forceinline__ void fft1024(S16 &s, const uint8_t *tabs, uint8_t *my, uint32_t lane) {
   asm volatile("" : "+v"(lane));
-  if constexpr (INDEX0) fpassC0(s, tabs);
-  else fpassC(s, tabs);
+  if constexpr (INDEX0) fpassC0<SM>(s, tabs);
+  else fpassC<SM>(s, tabs);
   exchange<LC, LB>(s, my, lane);
-  fpass4<4>(s, tabs, tlin((lane >> 4) << 8));
+  fpass4<4, SM>(s, tabs, tlin((lane >> 4) << 8));
   exchange<LB, LA>(s, my, lane);
-  fpass4<0>(s, tabs, tlin(16 * lane));
+  fpass4<0, SM>(s, tabs, tlin(16 * lane));
 }
 
 // ---- cross-lane helpers, layout bit maps, closed-form derivative and the
@@ -389,7 +446,7 @@ __device__ __forceinline__ void swap_bit(uint32_t &x, uint32_t &y, int b, bool h
   else y = recv;
 }
 
-template <Layout X, int L, int KB>
+template <Layout X, int L, int KB, int SM = kNoTower>
 __device__ __forceinline__ void fft_restricted(S16 &s, const uint8_t *tabs, uint32_t lane) {
   constexpr int F = X == LC ? 6 : 4;  // lowest register-held position bit
   constexpr int SB = swap_rbit<X>(), NL = lane_stages<X>();
@@ -400,9 +457,16 @@ __device__ __forceinline__ void fft_restricted(S16 &s, const uint8_t *tabs, uint
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       if (((r >> b) & 1) || !live_above<X, L, KB>(r, t)) continue;
-      Tab T;
-      tab_at(tabs, tlin(skew_idx(reg_pos<X, L>(r, -1), t)), T);
-      fb(s, r, r | (1 << b), T);
+      const uint32_t a = tlin(skew_idx(reg_pos<X, L>(r, -1), t));
+      if (t >= SM) {
+        SubTab T;
+        tab_at(tabs, a, T);
+        fb(s, r, r | (1 << b), T);
+      } else {
+        Tab T;
+        tab_at(tabs, a, T);
+        fb(s, r, r | (1 << b), T);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -420,9 +484,16 @@ __device__ __forceinline__ void fft_restricted(S16 &s, const uint8_t *tabs, uint
       const int r1 = r | (1 << SB);
       swap_bit(s.l[r], s.l[r1], u, hi);
       swap_bit(s.h[r], s.h[r1], u, hi);
-      Tab T;
-      tab_at(tabs, tlin(skew_idx((lane_hi | reg_pos<X, L>(r, SB)) & ((1u << L) - 1), u)), T);
-      fb(s, r, r1, T);
+      const uint32_t a = tlin(skew_idx((lane_hi | reg_pos<X, L>(r, SB)) & ((1u << L) - 1), u));
+      if (u >= SM) {
+        SubTab T;
+        tab_at(tabs, a, T);
+        fb(s, r, r1, T);
+      } else {
+        Tab T;
+        tab_at(tabs, a, T);
+        fb(s, r, r1, T);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
   }

@@ -102,6 +102,8 @@ int main() {
       const uint32_t idx = 1024 * q + i, c = f.skews[idx];
       if (__builtin_ctz(idx + 1) >= sub_min(q)) CHECK(c == kZeroTab || f.exp[c] < 256, "q=%d i=%u", q, i);
     }
+  // reconstruct_n4096's cross-quarter skews (dec_n4096.hip n4096_lin) are subfield
+  for (uint32_t i : {1023u, 2047u, 3071u}) CHECK(f.skews[i] == kZeroTab || f.exp[f.skews[i]] < 256, "skew %u", i);
   // IFFT / FFT of size 1024 at index 1024 q (additive_fft.hpp:99-141), in
   // symbols with mtab and in tower coordinates with the image rule
   for (int q = 0; q < 4; ++q)
