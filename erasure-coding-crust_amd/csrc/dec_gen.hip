@@ -37,12 +37,20 @@ __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ?
 // When the pass holds the top local bit (B0 + NS == L), the lane part of a
 // skew index has no bits above the stage, so a register block whose bits above
 // the stage are 0 (blk < 2d) has skew skews[d - 1] = 0xFFFF: b ^= a only.
+// Tower image 0: stages >= SM multiply with subfield tables.
+constexpr int SM = tower_sub_min(0);
 template <int B0, int NS, int L>
 __device__ __forceinline__ void ipassg(S16 &s, const uint8_t *tabs, uint32_t lb) {
   constexpr uint32_t NM = (1u << L) - 1;
   constexpr bool TOP = B0 + NS == L;
   Tab T[2];
-  tab_at(tabs, lb ^ tlin(skew_idx(0, B0)), T[0]);
+  SubTab U[2];
+  const auto fetch = [&](int t, int blk, int slot) __attribute__((always_inline)) {
+    const uint32_t a = lb ^ tlin(skew_idx((uint32_t(blk) << B0) & NM, B0 + t));
+    if (B0 + t >= SM) tab_at(tabs, a, U[slot]);
+    else tab_at(tabs, a, T[slot]);
+  };
+  fetch(0, 0, 0);
   int k = 0;
 #pragma unroll
   for (int t = 0; t < NS; ++t) {
@@ -50,11 +58,11 @@ __device__ __forceinline__ void ipassg(S16 &s, const uint8_t *tabs, uint32_t lb)
 #pragma unroll
     for (int blk = 0; blk < 16; blk += 2 * d, ++k) {
       const int nt = blk + 2 * d < 16 ? t : t + 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
-      if (nt < NS)
-        tab_at(tabs, lb ^ tlin(skew_idx((uint32_t(nblk) << B0) & NM, B0 + nt)), T[(k + 1) & 1]);
+      if (nt < NS) fetch(nt, nblk, (k + 1) & 1);
 #pragma unroll
       for (int i = 0; i < d; ++i) {
         if (TOP && ((blk << B0) & NM) >> (B0 + t + 1) == 0) bx(s, blk + i, blk + i + d);
+        else if (B0 + t >= SM) ib(s, blk + i, blk + i + d, U[k & 1]);
         else ib(s, blk + i, blk + i + d, T[k & 1]);
       }
     }
@@ -70,7 +78,7 @@ __device__ __forceinline__ void ipassCg(S16 &s, const uint8_t *tabs) {
 #pragma unroll
   for (int hi = 0; hi < 4; ++hi) bx(s, 4 * hi, 4 * hi + 1);
   if constexpr (L == 10) {
-    Tab Tb;
+    SubTab Tb;  // stage 8 >= SM
     tab_at(tabs, tlin(skew_idx(1u << 9, 8)), Tb);
 #pragma unroll
     for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi + 2, 4 * hi + 3, Tb);
@@ -106,7 +114,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
   const uint32_t tid0 = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid0 >> 6);
   uint8_t *my = regions + wave * REG_BYTES;
 
-  Tabs::copy_image<THREADS>(tabs, t.timg, tid0);  // skews 0..1022 (index 0)
+  Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);  // skews 0..1022 (index 0), tower image
   __syncthreads();
 
   // a contiguous range of tiles per workgroup, so consecutive tiles share a
@@ -152,14 +160,14 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
         const uint32_t e = order[b * N + slot];
         rv[rr] = e >> 16;
         rhave[rr] = (e & 0xffffu) != 0xffffu;
-        load_tab(t.mtab, rhave[rr] ? (e & 0xffffu) : 0u, RT[rr]);
+        load_tab(t.mtab_tin, rhave[rr] ? (e & 0xffffu) : 0u, RT[rr]);  // scaled into tower coordinates
       }
 #pragma unroll
       for (int it = 0; it < (128 * 5 + THREADS - 1) / THREADS; ++it) {  // k * 5 <= 640 chunks
         const uint32_t i = tid + it * THREADS;
         if (i < uint32_t(k) * 5)
           *reinterpret_cast<uint4 *>(outtabs + OutTabs::addr(i / 5, i % 5)) =
-              reinterpret_cast<const uint4 *>(t.mtab + mul_index(E[i / 5]))[i % 5];
+              reinterpret_cast<const uint4 *>(t.mtab_tout + mul_index(E[i / 5]))[i % 5];  // tower in
       }
     }
 
@@ -258,7 +266,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
       __builtin_amdgcn_sched_barrier(0);
       derivative<LB, L, KB>(s, lane);
       __builtin_amdgcn_sched_barrier(0);
-      fft_restricted<LB, L, KB>(s, tabs, lane);
+      fft_restricted<LB, L, KB, SM>(s, tabs, lane);
     } else {
       ipassg<4, 4, L>(s, tabs, lbB());
       __builtin_amdgcn_sched_barrier(0);
@@ -267,7 +275,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_gen(
       __builtin_amdgcn_sched_barrier(0);
       derivative<LC, L, KB>(s, lane);
       __builtin_amdgcn_sched_barrier(0);
-      fft_restricted<LC, L, KB>(s, tabs, lane);
+      fft_restricted<LC, L, KB, SM>(s, tabs, lane);
     }
     __builtin_amdgcn_s_setprio(0);
 #pragma unroll

@@ -24,6 +24,8 @@
 // lane chunks of contiguous row segments (64 * 1024 / k bytes).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "ec_kernels.hpp"
 #include "tf1024.hpp"
 
@@ -46,11 +48,18 @@ struct Geo {
 };
 
 // inverse pass over register bits 0..NS-1 = position bits B0..B0+NS-1
-template <int B0, int NS, int M>
+// SM: the tower image's first subfield stage
+template <int B0, int NS, int M, int SM>
 __device__ __forceinline__ void ipassg(S16 &s, const uint8_t *tabs, uint32_t lb) {
   constexpr uint32_t KM = Geo<M>::K - 1;
   Tab T[2];
-  tab_at(tabs, lb ^ tlin(skew_idx(0, B0)), T[0]);
+  SubTab U[2];
+  const auto fetch = [&](int t, int blk, int slot) __attribute__((always_inline)) {
+    const uint32_t a = lb ^ tlin(skew_idx((uint32_t(blk) << B0) & KM, B0 + t));
+    if (B0 + t >= SM) tab_at(tabs, a, U[slot]);
+    else tab_at(tabs, a, T[slot]);
+  };
+  fetch(0, 0, 0);
   int k = 0;
 #pragma unroll
   for (int t = 0; t < NS; ++t) {
@@ -58,19 +67,27 @@ __device__ __forceinline__ void ipassg(S16 &s, const uint8_t *tabs, uint32_t lb)
 #pragma unroll
     for (int blk = 0; blk < 16; blk += 2 * d, ++k) {
       const int nt = blk + 2 * d < 16 ? t : t + 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
-      if (nt < NS)
-        tab_at(tabs, lb ^ tlin(skew_idx((uint32_t(nblk) << B0) & KM, B0 + nt)), T[(k + 1) & 1]);
+      if (nt < NS) fetch(nt, nblk, (k + 1) & 1);
 #pragma unroll
-      for (int i = 0; i < d; ++i) ib(s, blk + i, blk + i + d, T[k & 1]);
+      for (int i = 0; i < d; ++i) {
+        if (B0 + t >= SM) ib(s, blk + i, blk + i + d, U[k & 1]);
+        else ib(s, blk + i, blk + i + d, T[k & 1]);
+      }
     }
   }
 }
 
-template <int B0, int NS, int M>
+template <int B0, int NS, int M, int SM>
 __device__ __forceinline__ void fpassg(S16 &s, const uint8_t *tabs, uint32_t lb) {
   constexpr uint32_t KM = Geo<M>::K - 1;
   Tab T[2];
-  tab_at(tabs, lb ^ tlin(skew_idx(0, B0 + NS - 1)), T[0]);
+  SubTab U[2];
+  const auto fetch = [&](int t, int blk, int slot) __attribute__((always_inline)) {
+    const uint32_t a = lb ^ tlin(skew_idx((uint32_t(blk) << B0) & KM, B0 + t));
+    if (B0 + t >= SM) tab_at(tabs, a, U[slot]);
+    else tab_at(tabs, a, T[slot]);
+  };
+  fetch(NS - 1, 0, 0);
   int k = 0;
 #pragma unroll
   for (int t = NS - 1; t >= 0; --t) {
@@ -78,10 +95,12 @@ __device__ __forceinline__ void fpassg(S16 &s, const uint8_t *tabs, uint32_t lb)
 #pragma unroll
     for (int blk = 0; blk < 16; blk += 2 * d, ++k) {
       const int nt = blk + 2 * d < 16 ? t : t - 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
-      if (nt >= 0)
-        tab_at(tabs, lb ^ tlin(skew_idx((uint32_t(nblk) << B0) & KM, B0 + nt)), T[(k + 1) & 1]);
+      if (nt >= 0) fetch(nt, nblk, (k + 1) & 1);
 #pragma unroll
-      for (int i = 0; i < d; ++i) fb(s, blk + i, blk + i + d, T[k & 1]);
+      for (int i = 0; i < d; ++i) {
+        if (B0 + t >= SM) fb(s, blk + i, blk + i + d, U[k & 1]);
+        else fb(s, blk + i, blk + i + d, T[k & 1]);
+      }
     }
   }
 }
@@ -95,14 +114,14 @@ __device__ __forceinline__ uint32_t lbB(uint32_t lane) {
 // k = 512, layout C: stage 8 (register bit 0); its skew index 255 (+ offset)
 // is uniform since p9 is an instance bit
 __device__ __forceinline__ void ipassC9(S16 &s, const uint8_t *tabs, uint32_t lo) {
-  Tab T;
+  SubTab T;  // stage 8: subfield in every tower image
   tab_at(tabs, lo ^ tlin(skew_idx(0, 8)), T);
 #pragma unroll
   for (int r = 0; r < 16; r += 2) ib(s, r, r + 1, T);
 }
 
 __device__ __forceinline__ void fpassC9(S16 &s, const uint8_t *tabs, uint32_t lo) {
-  Tab T;
+  SubTab T;
   tab_at(tabs, lo ^ tlin(skew_idx(0, 8)), T);
 #pragma unroll
   for (int r = 0; r < 16; r += 2) fb(s, r, r + 1, T);
@@ -172,10 +191,11 @@ __global__ void __launch_bounds__(THREADS)
   int img = 0;  // table image in LDS: skews 1024 img .. + 1022
   const auto load_image = [&](int q) {
     lds_barrier();  // every wave is done with the current tables
-    Tabs::copy_image<THREADS>(tabs, t.timg + q * kTabImageBytes, tid0);
+    Tabs::copy_image<THREADS>(tabs, t.timg_t + q * kTabImageBytes, tid0);
     lds_barrier();
   };
-  Tabs::copy_image<THREADS>(tabs, t.timg, tid0);  // skews 0..1022: every coset of n <= 1024
+  // tower images: the transforms run in tower coordinates
+  Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);  // skews 0..1022: every coset of n <= 1024
   __syncthreads();
 
   const uint64_t npieces = slen / 2;
@@ -232,6 +252,11 @@ __global__ void __launch_bounds__(THREADS)
     stage<M>(s, my, lane);
     lds_barrier();
     store_rows<M>(regions, SH, sstride, 0, nv, piece0, npieces, tid);
+    {  // into tower coordinates
+      const TowerK tk = tower_k();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s.l[r] = tower_lo(s.l[r], s.h[r], tk);
+    }
 
     // ---- IFFT_k (index 0): pass A, exchange, pass B -> layout B
     if (img != 0) {  // the previous tile ended on a higher image
@@ -239,23 +264,42 @@ __global__ void __launch_bounds__(THREADS)
       img = 0;
     }
     const uint32_t lbA = tlin((16 * lane) & (Gm::K - 1));
-    ipassg<0, (M < 4 ? M : 4), M>(s, tabs, lbA);
+    constexpr int S0 = tower_sub_min(0);
+    ipassg<0, (M < 4 ? M : 4), M, S0>(s, tabs, lbA);
     if constexpr (M == 4) {
       // k = 16: the whole IFFT is pass A; coefficients stay in layout A
     } else if constexpr (M <= 8) {
       lds_barrier();  // systematic rows read out of the regions
       exchange<LA, LB>(s, my, lane);
-      ipassg<4, M - 4, M>(s, tabs, 0);
+      ipassg<4, M - 4, M, S0>(s, tabs, 0);
     } else {
       lds_barrier();  // systematic rows read out of the regions
       exchange<LA, LB>(s, my, lane);
-      ipassg<4, 4, M>(s, tabs, lbB(lane));
+      ipassg<4, 4, M, S0>(s, tabs, lbB(lane));
       exchange<LB, LC>(s, my, lane);
       ipassC9(s, tabs, 0);
     }
     const S16 coef = s;
 
     // ---- FFT_k at each coset shift (encodeLow, poly_encoder.hpp:229-237)
+    // coset FFT with tower image img's first subfield stage SMv (integral_constant)
+    const auto coset_fft = [&](auto smv, const uint32_t lo) __attribute__((always_inline)) {
+      constexpr int SMc = decltype(smv)::value;
+      if constexpr (M == 4) {
+        lds_barrier();  // previous rows read out of the regions
+      } else if constexpr (M <= 8) {
+        fpassg<4, M - 4, M, SMc>(s, tabs, lo);
+        lds_barrier();  // previous rows read out of the regions
+        exchange<LB, LA>(s, my, lane);
+      } else {
+        fpassC9(s, tabs, lo);
+        lds_barrier();  // previous rows read out of the regions
+        exchange<LC, LB>(s, my, lane);
+        fpassg<4, 4, M, SMc>(s, tabs, lbB(lane) ^ lo);
+        exchange<LB, LA>(s, my, lane);
+      }
+      fpassg<0, (M < 4 ? M : 4), M, SMc>(s, tabs, tlin((16 * lane) & (Gm::K - 1)) ^ lo);
+    };
     for (int sh = int(Gm::K); sh < n && sh < nv; sh += int(Gm::K)) {
       if ((sh >> 10) != img) {  // (load_image waits for every wave's last table reads)
         img = sh >> 10;
@@ -265,20 +309,14 @@ __global__ void __launch_bounds__(THREADS)
 #pragma unroll
       for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(s.l[r]), "+v"(s.h[r]));
       const uint32_t lo = tlin(uint32_t(sh) & 1023u);  // tables at offset sh (disjoint bits)
-      if constexpr (M == 4) {
-        lds_barrier();  // previous rows read out of the regions
-      } else if constexpr (M <= 8) {
-        fpassg<4, M - 4, M>(s, tabs, lo);
-        lds_barrier();  // previous rows read out of the regions
-        exchange<LB, LA>(s, my, lane);
-      } else {
-        fpassC9(s, tabs, lo);
-        lds_barrier();  // previous rows read out of the regions
-        exchange<LC, LB>(s, my, lane);
-        fpassg<4, 4, M>(s, tabs, lbB(lane) ^ lo);
-        exchange<LB, LA>(s, my, lane);
+      if (img == 0) coset_fft(std::integral_constant<int, tower_sub_min(0)>(), lo);
+      else if (img == 1) coset_fft(std::integral_constant<int, tower_sub_min(1)>(), lo);
+      else coset_fft(std::integral_constant<int, tower_sub_min(2)>(), lo);  // images 2, 3
+      {  // back to symbol coordinates
+        const TowerK tk = tower_k();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s.l[r] = tower_lo(s.l[r], s.h[r], tk);
       }
-      fpassg<0, (M < 4 ? M : 4), M>(s, tabs, tlin((16 * lane) & (Gm::K - 1)) ^ lo);
       stage<M>(s, my, lane);  // own region: no other wave touches it since the barrier above
       lds_barrier();
       store_rows<M>(regions, SH, sstride, uint32_t(sh), nv, piece0, npieces, tid);
