@@ -66,7 +66,11 @@ __device__ __forceinline__ void lds_tab_at(const uint8_t *lds, uint32_t lin, Tab
 
 // subfield table (tower image): plane 0 and dword 0 of plane 1
 __device__ __forceinline__ void lds_tab_at(const uint8_t *lds, uint32_t lin, SubTab &T) {
+#ifdef DIAG_SUB_NOCONFLICT  // diagnostic builds only (wrong results): conflict-free plane-1 reads
+  T.t[4] = *reinterpret_cast<const uint32_t *>(lds + Tabs::kPlane + 4 * __builtin_amdgcn_mbcnt_lo(~0u, 0));
+#else
   T.t[4] = *reinterpret_cast<const uint32_t *>(lds + Tabs::kPlane + lin);
+#endif
   const uint4 v = *reinterpret_cast<const uint4 *>(lds + lin);
   T.t[0] = v.x;
   T.t[1] = v.y;
@@ -124,17 +128,38 @@ __device__ __forceinline__ void fbfly(State &s, int ra, int rb, const T &Tb) {
 // table load in flight instead of stalling on each (2 x 20 VGPRs).
 // radix-8 pass over 3 consecutive position bits b0..b0+2 held in registers:
 // pos(r) = base | (r << b0).  Inverse: stages b0, b0+1, b0+2.
-// Stages >= SM (the tower image's subfield stages) multiply with SubTab.
-template <int b0, int SM>
+// Stages >= SM (the tower image's subfield stages) multiply with SubTab, and
+// so do stages SL <= m < SM, whose skews the caller knows to be subfield too:
+// those read the stage-2 slot of the same element, 2 ((off | pos) >> (m + 1))
+// (alias index ((off | pos) >> (m + 1)) << 3 | 3).
+template <int b0, int SM, int SL>
+struct PassIdx {
+  static constexpr bool A0 = b0 < SM && b0 >= SL, A1 = b0 + 1 < SM && b0 + 1 >= SL;
+  uint32_t lb, la0, la1, off;
+  __device__ __forceinline__ PassIdx(uint32_t base, uint32_t off_) : off(off_) {
+    lb = tlin(base & ~((2u << b0) - 1));  // lane part of every index below
+    la0 = A0 ? tlin(((base | off) >> (b0 + 1)) << 3) : 0u;
+    la1 = A1 ? tlin(((base | off) >> (b0 + 2)) << 3) : 0u;
+  }
+  __device__ __forceinline__ uint32_t i0(int rr) const {
+    return A0 ? la0 ^ tlin((uint32_t(rr) << 3) | 3u) : lb ^ tlin(skew_idx(uint32_t(2 * rr) << b0, b0, off));
+  }
+  __device__ __forceinline__ uint32_t i1(int hh) const {
+    return A1 ? la1 ^ tlin((uint32_t(hh) << 3) | 3u) : lb ^ tlin(skew_idx(uint32_t(4 * hh) << b0, b0 + 1, off));
+  }
+  __device__ __forceinline__ uint32_t i2() const { return lb ^ tlin(skew_idx(0, b0 + 2, off)); }
+};
+
+template <int b0, int SM, int SL = SM>
 __device__ __forceinline__ void ipass3(State &s, const uint8_t *tabs, uint32_t base, uint32_t off) {
   {
-    TabAt<b0, SM> Ta0, Tb0;
-    TabAt<b0 + 1, SM> Ta1, Tb1;
-    TabAt<b0 + 2, SM> Ta2;
-    const uint32_t lb = tlin(base & ~((2u << b0) - 1));  // lane part of every index below
-    const auto i0 = [&](int rr) { return lb ^ tlin(skew_idx(uint32_t(2 * rr) << b0, b0, off)); };
-    const auto i1 = [&](int hh) { return lb ^ tlin(skew_idx(uint32_t(4 * hh) << b0, b0 + 1, off)); };
-    const uint32_t i2 = lb ^ tlin(skew_idx(0, b0 + 2, off));
+    TabAt<b0, SL> Ta0, Tb0;
+    TabAt<b0 + 1, SL> Ta1, Tb1;
+    TabAt<b0 + 2, SL> Ta2;
+    const PassIdx<b0, SM, SL> ix(base, off);
+    const auto i0 = [&](int rr) { return ix.i0(rr); };
+    const auto i1 = [&](int hh) { return ix.i1(hh); };
+    const uint32_t i2 = ix.i2();
     lds_tab_at(tabs, i0(0), Ta0);
     lds_tab_at(tabs, i0(1), Tb0);
     ibfly(s, 0, 1, Ta0);
@@ -156,16 +181,16 @@ __device__ __forceinline__ void ipass3(State &s, const uint8_t *tabs, uint32_t b
 }
 
 // forward: stages b0+2, b0+1, b0
-template <int b0, int SM>
+template <int b0, int SM, int SL = SM>
 __device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t base, uint32_t off) {
   {
-    TabAt<b0, SM> Ta0, Tb0;
-    TabAt<b0 + 1, SM> Ta1, Tb1;
-    TabAt<b0 + 2, SM> Ta2;
-    const uint32_t lb = tlin(base & ~((2u << b0) - 1));  // lane part of every index below
-    const auto i0 = [&](int rr) { return lb ^ tlin(skew_idx(uint32_t(2 * rr) << b0, b0, off)); };
-    const auto i1 = [&](int hh) { return lb ^ tlin(skew_idx(uint32_t(4 * hh) << b0, b0 + 1, off)); };
-    const uint32_t i2 = lb ^ tlin(skew_idx(0, b0 + 2, off));
+    TabAt<b0, SL> Ta0, Tb0;
+    TabAt<b0 + 1, SL> Ta1, Tb1;
+    TabAt<b0 + 2, SL> Ta2;
+    const PassIdx<b0, SM, SL> ix(base, off);
+    const auto i0 = [&](int rr) { return ix.i0(rr); };
+    const auto i1 = [&](int hh) { return ix.i1(hh); };
+    const uint32_t i2 = ix.i2();
     lds_tab_at(tabs, i2, Ta2);
     lds_tab_at(tabs, i1(0), Tb1);
 #pragma unroll
@@ -587,7 +612,8 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
         img = 0;
       }
     }
-    ipass3<0, tower_sub_min(0)>(s, tabs, posA(q, 0), 0);
+    // index 0, positions < 256: every skew is subfield (stages 0, 1 by alias)
+    ipass3<0, tower_sub_min(0), 0>(s, tabs, posA(q, 0), 0);
     rsync();  // systematic rows read out of the regions
     exchange<LA, LB>(s, xch, xb);
     ipass3<3, tower_sub_min(0)>(s, tabs, posB(q, 0), 0);
@@ -597,8 +623,9 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
 
     // ---- FFT_256 at each coset shift (encodeLow, poly_encoder.hpp:229-237)
     // sm: the tower image's first subfield stage (std::integral_constant)
-    const auto coset = [&](auto sm, const uint32_t sh, const uint32_t off) __attribute__((always_inline)) {
-      constexpr int SM = decltype(sm)::value;
+    // sl: first subfield stage of this coset's pass A (<= SM: aliased stages)
+    const auto coset = [&](auto sm, auto sl, const uint32_t sh, const uint32_t off) __attribute__((always_inline)) {
+      constexpr int SM = decltype(sm)::value, SL = decltype(sl)::value;
       s = coef;
       // opaque copy: keeps the compiler from hoisting the first stage's selector
       // masks out of the coset loop (that costs ~50 VGPRs and forces spills)
@@ -611,7 +638,7 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
       exchange<LC, LB>(s, xch, xb);
       fpass3<3, SM>(s, tabs, posB(q, 0), off);
       exchange<LB, LA>(s, xch, xb);
-      fpass3<0, SM>(s, tabs, posA(q, 0), off);
+      fpass3<0, SM, SL>(s, tabs, posA(q, 0), off);
       {  // back to symbol coordinates
         const TowerK tk = tower_k();
 #pragma unroll
@@ -624,14 +651,16 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     };
     using Sub0 = std::integral_constant<int, tower_sub_min(0)>;
     using Sub1 = std::integral_constant<int, tower_sub_min(1)>;
-    for (uint32_t sh = K; sh < 1024u && int(sh) < nv; sh += K) coset(Sub0(), sh, sh);
+    // coset 1 (index 256): stage 1 skews are 128 + 2 (pos >> 2), subfield
+    coset(Sub0(), std::integral_constant<int, 1>(), K, K);  // (nv > 256 for k = 256)
+    for (uint32_t sh = 2 * K; sh < 1024u && int(sh) < nv; sh += K) coset(Sub0(), Sub0(), sh, sh);
     if constexpr (N > 1024) {
       for (uint32_t sh = 1024u; sh < uint32_t(N) && int(sh) < nv; sh += K) {
         if (sh == 1024u) {
           load_image(1);
           img = 1;
         }
-        coset(Sub1(), sh, sh & 1023u);
+        coset(Sub1(), Sub1(), sh, sh & 1023u);
       }
     }
   }

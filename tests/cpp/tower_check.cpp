@@ -102,6 +102,20 @@ int main() {
       const uint32_t idx = 1024 * q + i, c = f.skews[idx];
       if (__builtin_ctz(idx + 1) >= sub_min(q)) CHECK(c == kZeroTab || f.exp[c] < 256, "q=%d i=%u", q, i);
     }
+  // alias slots (enc_k256.hip PassIdx, dec_n1024.hip sub_alias): the skew of
+  // position p at stage m of the transform at index off (a multiple of 2^(m+1))
+  // has element 2 ((off | p) >> (m + 1)); the stage-2 slot
+  // ((off | p) >> (m + 1)) << 3 | 3 holds the same element
+  for (uint32_t m = 0; m < 10; ++m)
+    for (uint32_t off = 0; off < 1024; off += (2u << m))
+      for (uint32_t p = 0; p < 1024 && off + p < 1024; ++p) {
+        const uint32_t h = (off | p) >> (m + 1);
+        if (h >= 128 || (off & p)) continue;
+        const uint32_t d = 1u << m, idx = ((off | p) & ~(2 * d - 1)) + d - 1, al = (h << 3) | 3;
+        const uint32_t c0 = f.skews[idx], c1 = f.skews[al];
+        const uint32_t e0 = c0 == kZeroTab ? 0 : f.exp[c0], e1 = c1 == kZeroTab ? 0 : f.exp[c1];
+        CHECK(e0 == e1 && e0 == 2 * h && __builtin_ctz(al + 1) == 2, "alias m=%u off=%u p=%u", m, off, p);
+      }
   // reconstruct_n4096's cross-quarter skews (dec_n4096.hip n4096_lin) are subfield
   for (uint32_t i : {1023u, 2047u, 3071u}) CHECK(f.skews[i] == kZeroTab || f.exp[f.skews[i]] < 256, "skew %u", i);
   // IFFT / FFT of size 1024 at index 1024 q (additive_fft.hpp:99-141), in
