@@ -37,7 +37,7 @@ constexpr size_t kMaxGrid = 1024;  // workgroups of the launch (>= the CU count)
 
 // own-region staging slot of row v (0..511) of wave w: the 8 lanes reading one
 // row from the 8 regions hit 8 distinct 16-B slots
-__device__ __forceinline__ uint32_t soff(uint32_t v, uint32_t w) {
+__host__ __device__ constexpr uint32_t soff(uint32_t v, uint32_t w) {
   return ((v >> 4) << 8) | (((v ^ (v >> 4) ^ w) & 15) << 4);
 }
 
@@ -61,6 +61,24 @@ __device__ __forceinline__ void store_half(const uint8_t *regions, uint8_t *SH, 
   const uint64_t p = piece0 + 8 * c;
   const bool wide = ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0;  // 16-B aligned rows
   const uint8_t *src = regions + c * REG_BYTES;
+  // the common case, decided once (uniform): aligned rows, the whole tile inside
+  // the payload, all 512 rows below n_validators -- one aligned 16-B store per
+  // lane and row, no per-lane tests (the general loop below compiles to a 4-B +
+  // a misaligned 12-B store per chunk)
+  if (wide && piece0 + TILE <= npieces && int(row0) + 512 <= nv) {
+    const uint32_t v0 = wave * 8 + (lane >> 3);
+    const uint32_t sa = lds_addr(src) + soff(v0, c);
+    uint8_t *dst = SH + uint64_t(row0 + v0) * sstride + 2 * p;
+    const uint64_t dstep = uint64_t(8 * WAVES) * sstride;
+#pragma unroll
+    for (int it = 0; it < 512 / (8 * WAVES); ++it) {  // soff is GF(2)-linear in v = it * 8 WAVES | v0
+      typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+      const v4u val = *(const __attribute__((address_space(3))) v4u *)(uintptr_t(sa ^ soff(uint32_t(it) * 8 * WAVES, 0)));
+      // streaming (non-temporal): rows are written once, not re-read
+      __builtin_nontemporal_store(val, reinterpret_cast<v4u *>(dst + it * dstep));
+    }
+    return;
+  }
 #pragma unroll 2
   for (int it = 0; it < 512 / (8 * WAVES); ++it) {
     const uint32_t v = uint32_t(it) * 8 * WAVES + wave * 8 + (lane >> 3);

@@ -322,7 +322,7 @@ __device__ __forceinline__ uint2 to_be(uint32_t l, uint32_t h) {
 // read one row from the 16 regions hit 16 distinct slots (conflict free) and
 // the layout-A writes are 2-way.  A wave only ever writes its own region, so
 // the next write needs a barrier only after the other waves' row reads.
-__device__ __forceinline__ uint32_t soff(uint32_t v, uint32_t w) {
+__host__ __device__ constexpr uint32_t soff(uint32_t v, uint32_t w) {
   return ((v >> 4) << 8) | (((v ^ (v >> 4) ^ w) & 15) << 4);
 }
 
@@ -368,12 +368,44 @@ __device__ __forceinline__ void store_chunk_any(uint8_t *dst, const uint4 val, u
 // piece0 + 8c of the tile's payload (SH), or, packed, pieces [pc, pc + 8) of
 // the payload bc that owns flattened slot tile * TILE + 8c (computed here, not
 // kept live across the FFTs)
+// The common case of store_own, decided once (uniform): 16-B aligned rows, the
+// whole tile inside the payload and all 256 rows below n_validators -- one
+// aligned 16-B streaming store per lane and row, addresses stepped, no
+// per-lane tests (the general form made the compiler merge its two store
+// shapes into a 4-B + a misaligned 12-B store per chunk)
+__device__ __forceinline__ bool rows_fast_ok(const uint8_t *SH, uint64_t sstride, uint32_t s0, int nv,
+                                             uint64_t piece0, uint64_t npieces) {
+  return ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0 && piece0 + TILE <= npieces &&
+         int(s0) + 256 <= nv;
+}
+__device__ __forceinline__ void store_rows_fast(const uint8_t *xbase, uint8_t *SH, uint64_t sstride,
+                                                uint32_t s0, uint64_t piece0, uint32_t wave, uint32_t lane) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const uint32_t c = lane & 15;
+  const uint32_t v0 = wave * 4 + (lane >> 4);
+  const uint32_t sa = lds_addr(xbase + c * XCH_BYTES) + soff(v0, c);
+  uint8_t *dst = SH + uint64_t(s0 + v0) * sstride + 2 * (piece0 + 8 * c);
+  const uint64_t dstep = uint64_t(4 * WAVES) * sstride;
+#pragma unroll
+  for (int it = 0; it < 256 / (4 * WAVES); ++it) {  // soff is GF(2)-linear in v = it * 4 WAVES | v0
+    const v4u val = *(const __attribute__((address_space(3))) v4u *)(uintptr_t(sa ^ soff(uint32_t(it) * 4 * WAVES, 0)));
+    // streaming (non-temporal): rows are written once, not re-read
+    __builtin_nontemporal_store(val, reinterpret_cast<v4u *>(dst + it * dstep));
+  }
+}
+
 template <bool PACKED>
 __device__ __forceinline__ void store_own(const uint8_t *xbase, uint8_t *SH, uint64_t sstride,
                                           uint32_t s0, int nv, uint64_t piece0, uint64_t npieces,
                                           uint32_t wave, uint32_t lane, uint64_t tile, uint32_t npp8,
                                           uint32_t batch) {
   asm volatile("" : "+v"(lane));  // recomputed here, not kept live across the FFTs
+  if constexpr (!PACKED) {
+    if (rows_fast_ok(SH, sstride, s0, nv, piece0, npieces)) {
+      store_rows_fast(xbase, SH, sstride, s0, piece0, wave, lane);
+      return;
+    }
+  }
   const uint32_t c = lane & 15;
   uint64_t p = piece0 + 8 * c;
   if constexpr (PACKED) {
