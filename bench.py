@@ -64,7 +64,8 @@ def pmc_traffic(kernel, nv, plen, cnt, batch):
 # waves per SIMD of the dominant kernels (launch shapes in csrc/): the SQ
 # counters' per-wave ACTIVE_INST_ANY fraction times this is the share of SIMD
 # cycles that issued an instruction
-_WAVES_PER_SIMD = {"reconstruct": ("reconstruct_n1024", 2), "encode": ("encode_k256<1024>", 4)}
+_WAVES_PER_SIMD = {"reconstruct": (("reconstruct_n1024<false>", "reconstruct_n1024"), 2),
+                   "encode": (("encode_k256<1024, 0>", "encode_k256<1024>"), 4)}
 
 
 def sq_issue(kernel, nv):
@@ -73,18 +74,19 @@ def sq_issue(kernel, nv):
     on the default workload shape (nv = 1024): the kernels are bounded by
     instruction issue, not HBM."""
     import glob
-    name, waves = _WAVES_PER_SIMD.get(kernel, (None, 0))
-    if name is None or nv != 1024:
+    names, waves = _WAVES_PER_SIMD.get(kernel, (None, 0))
+    if names is None or nv != 1024:
         return None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "sq_counters.json")),
                        reverse=True):
         try:
             with open(path) as f:
-                k = json.load(f)["kernels"][name]
+                ks = json.load(f)["kernels"]
+            k = next(ks[n] for n in names if n in ks)  # (kernel names by round)
             return {"simd_issue_frac": round(k["frac_active_inst_any"] * waves, 3),
                     "valu_frac": round(k["frac_active_valu"] * waves, 3),
                     "source": os.path.relpath(path, ROOT)}
-        except (OSError, KeyError, ValueError):
+        except (OSError, KeyError, ValueError, StopIteration):
             continue
     return None
 
