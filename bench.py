@@ -346,6 +346,8 @@ def main():
                          "n_validators=nv and report them in `sizes`; 'none': skip; or a comma list")
     ap.add_argument("--sweep-cpu-seconds", type=float, default=0.5,
                     help="ec-cpp sample per size and thread count in the sweep")
+    ap.add_argument("--row-align", type=int, default=64,
+                    help="device shard row stride = shard_len rounded up to this many bytes")
     ap.add_argument("--graph", action="store_true",
                     help="time K replays of one captured hipGraph step (ECCR_AMD_*_ws calls on "
                          "caller-owned scratch) instead of K eager steps")
@@ -375,7 +377,7 @@ def main():
     n, k, thr = E.code_params(nv)
     cnt = {"threshold": thr, "k": k}.get(args.present) or int(args.present)
     sl = E.shard_len(nv, plen)
-    ss = (sl + 63) // 64 * 64  # device shard row stride (aligned rows)
+    ss = (sl + args.row_align - 1) // args.row_align * args.row_align  # device shard row stride
     dev = torch.device("cuda", local)
 
     # synthetic inputs, resident before timing; seeds are global payload indices

@@ -575,6 +575,50 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     const uint8_t *P = payloads + b * pstride;
     uint8_t *SH = PACKED ? shards : shards + b * uint64_t(nv) * sstride;  // packed: per chunk
 
+    const auto store = [&](uint32_t s0) __attribute__((always_inline)) {
+      if constexpr (PK == 2)
+        store_wave(xch, shards, sstride, s0, nv, uint32_t(tile), uint32_t(npieces), batch, wave, lane);
+      else
+        store_own<PACKED>(stg, SH, sstride, s0, nv, piece0, npieces, wave, lane, tile, npp8, batch);
+    };
+
+    // A wave none of whose 8 pieces exist (the last, partial tile of a payload:
+    // 1 MB is 1953 pieces, its 16th tile has 33) skips the transforms and only
+    // takes part in the barriers, the image loads and the row stores of the
+    // others, in the same order as below (wave-uniform branch)
+    if constexpr (PK == 0) {
+      if (piece0 + 8 * wave_s >= npieces) {
+        rsync();  // tile start
+        rsync();  // systematic rows staged
+        store(0);
+        if constexpr (N > 1024) {
+          if (img != 0) {
+            load_image(0);
+            img = 0;
+          }
+        }
+        rsync();  // after IFFT pass A
+        const auto coset_idle = [&](uint32_t sh) __attribute__((always_inline)) {
+          rsync();  // after pass C
+          rsync();  // rows staged
+          store(sh);
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        coset_idle(K);
+        for (uint32_t sh = 2 * K; sh < 1024u && int(sh) < nv; sh += K) coset_idle(sh);
+        if constexpr (N > 1024) {
+          for (uint32_t sh = 1024u; sh < uint32_t(N) && int(sh) < nv; sh += K) {
+            if (sh == 1024u) {
+              load_image(1);
+              img = 1;
+            }
+            coset_idle(sh);
+          }
+        }
+        continue;
+      }
+    }
+
     // ---- load 8 pieces x 16 bytes (positions 8q..8q+7), zero past plen
     State s;
 #pragma unroll
@@ -620,12 +664,6 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     }
 
     // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)
-    const auto store = [&](uint32_t s0) __attribute__((always_inline)) {
-      if constexpr (PK == 2)
-        store_wave(xch, shards, sstride, s0, nv, uint32_t(tile), uint32_t(npieces), batch, wave, lane);
-      else
-        store_own<PACKED>(stg, SH, sstride, s0, nv, piece0, npieces, wave, lane, tile, npp8, batch);
-    };
     rsync();  // the other waves are done reading this region (last tile)
     stage_own(s, xch, q, inst, wave);
     rsync();
