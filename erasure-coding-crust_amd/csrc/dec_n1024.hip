@@ -489,12 +489,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
           w[half][4 * q + 2] = d.z;
           w[half][4 * q + 3] = d.w;
         }
-      } else {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) w[half][q] = 0;
-#pragma unroll
-        for (int e = 0; e < 64; ++e)  // constant trip count: w stays in registers
-          if (uint64_t(e) < avail) w[half][e >> 2] |= uint32_t(row[e]) << (8 * (e & 3));
+      } else {  // the payload's last tile: whole dwords, then bytes (rows 16-B aligned here)
+        load_row_tail64(row, avail, w[half]);
       }
       load_tab(t.mtab_tin, meta[half] & 0xffffu, RT[half]);  // scaled into tower coordinates
     };
@@ -535,10 +531,20 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     STAMP(2);
     if constexpr (!PACKED) __syncthreads();  // packed: the wave's own region and staging only
     STAMP(3);
+    const uint64_t cbase = col0 + 4 * wave;
+    if constexpr (!PACKED) {
+      // a group past the payload's last column (its last, partial tile: 1 MB
+      // shards are 977 columns, the 31st tile has 17): phases 2-5 are this
+      // wave's alone, so it goes straight to the next tile's barrier
+      if (col0 + 4 * uint64_t(wave_s) >= ncols) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) meta[i] = meta_next[i];
+        continue;
+      }
+    }
     // phase-5 tables requested now, consumed after the transform (latency
     // hidden behind it): E[y] of this lane's erased output rows y = 4 lane + q
     // (its present ones are in the staging area)
-    const uint64_t cbase = col0 + 4 * wave;
     Tab T5[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {

@@ -141,6 +141,10 @@ reconstruct_n4096(
     const uint16_t *E = elog + pt * N;
     uint8_t *O = out + b * ostride;
     S16 P, Qa;  // the two accumulators of the linearised cross-quarter stages
+    // a wave whose 4 columns lie past the payload's last one (its last, partial
+    // tile: 1 MB at k = 1024 is 489 columns, the 16th tile has 9) gathers with
+    // the others but skips its transforms and output (uniform)
+    const bool idle = col0 + 4 * wave >= ncols;
     // this thread's two gather slots of a quarter (gather_order, dec_n1024.hip:
     // present rows first, dealt wave-major): (row in quarter << 16) |
     // mul_index(E[row]), low half 0xFFFF = absent.  The next quarter's are
@@ -216,19 +220,21 @@ reconstruct_n4096(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // table image landed
       lds_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      const uint32_t la = region_lane<LA>(my, lq);
+      if (!idle) {
+        const uint32_t la = region_lane<LA>(my, lq);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const uint2 x = lds_ld2(region_at<LA>(la, r));
-        Qq.l[r] = x.x;
-        Qq.h[r] = x.y;
+        for (int r = 0; r < 16; ++r) {
+          const uint2 x = lds_ld2(region_at<LA>(la, r));
+          Qq.l[r] = x.x;
+          Qq.h[r] = x.y;
+        }
+        // the two waves of a SIMD (w, w + 4) alternate the higher issue
+        // priority from quarter to quarter (as reconstruct_n1024's passes)
+        if (((wave >> 2) ^ uint32_t(q)) & 1) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(0);
+        // -> layout C; quarter 0 is at index 0
+        ifft1024<q == 0, tower_sub_min(q)>(Qq, tabs, my, lq);
       }
-      // the two waves of a SIMD (w, w + 4) alternate the higher issue
-      // priority from quarter to quarter (as reconstruct_n1024's passes)
-      if (((wave >> 2) ^ uint32_t(q)) & 1) __builtin_amdgcn_s_setprio(2);
-      else __builtin_amdgcn_s_setprio(0);
-      // -> layout C; quarter 0 is at index 0
-      ifft1024<q == 0, tower_sub_min(q)>(Qq, tabs, my, lq);
       __builtin_amdgcn_sched_barrier(0);
       if (qnext >= 0) {  // the next quarter's first row and tables
         if (has(0)) load_row(qnext, 0, w0, RT0);
@@ -243,6 +249,7 @@ reconstruct_n4096(
       // Qa is read at the registers reaching y < k only; P also at their
       // single-bit partners (the derivative): everywhere but r & 3 == 3
       // (p8 = p9 = 1) when k = 256.
+      if (idle) return;
       uint32_t ip = lin.p[q], ik = lin.k[q];
       asm volatile("" : "+s"(ip), "+s"(ik));  // loaded here, not hoisted (and kept live) from the top
       if (ip == 0) {
@@ -304,21 +311,23 @@ reconstruct_n4096(
     // D in closed form (poly_encoder.hpp:195-215) over bits 0..9, in place:
     // lane = p0..p5, r = (p8, p9, p6, p7).
     __builtin_amdgcn_s_setprio(0);
-    derivative<LC, 10, KB>(P, lane);  // at the registers reaching y < k only
     S16 Y;
+    if (!idle) {
+      derivative<LC, 10, KB>(P, lane);  // at the registers reaching y < k only
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      Y.l[r] = P.l[r] ^ Qa.l[r];
-      Y.h[r] = P.h[r] ^ Qa.h[r];
-    }
+      for (int r = 0; r < 16; ++r) {
+        Y.l[r] = P.l[r] ^ Qa.l[r];
+        Y.h[r] = P.h[r] ^ Qa.h[r];
+      }
 
-    // ---- FFT_1024, index 0 (quarter 0's tables still resident): whole for
-    // k = 1024 (-> layout A: y = 16 lane + r), else restricted to y < k
-    // (tf1024.hpp fft_restricted: live register pairs hold y0, y0 + 1)
-    if constexpr (KB == 10) fft1024<true, tower_sub_min(0)>(Y, tabs, my, lane);
-    else fft_restricted<LC, 10, KB, tower_sub_min(0)>(Y, tabs, lane);
+      // ---- FFT_1024, index 0 (quarter 0's tables still resident): whole for
+      // k = 1024 (-> layout A: y = 16 lane + r), else restricted to y < k
+      // (tf1024.hpp fft_restricted: live register pairs hold y0, y0 + 1)
+      if constexpr (KB == 10) fft1024<true, tower_sub_min(0)>(Y, tabs, my, lane);
+      else fft_restricted<LC, 10, KB, tower_sub_min(0)>(Y, tabs, lane);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(Y.l[r]), "+v"(Y.h[r]));  // not sunk past the table gather
+      for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(Y.l[r]), "+v"(Y.h[r]));  // not sunk past the table gather
+    }
 
     // ---- output (decode_main:185-188, reconstructSub:138-149): erased y < k
     // scaled by E[y] (tables now in LDS), present y copied from the shard
@@ -334,6 +343,7 @@ reconstruct_n4096(
           tabs, t.mtab_tout, [&](uint32_t y) { return mul_index(E[y]); },  // tower in, symbols out
           [&](uint32_t y) { return y < K; }, [&](uint32_t y) { return !(int(y) < nv && pr[y]); }, tid);
     lds_barrier();
+    if (idle) continue;
     if constexpr (KB < 10) {
       constexpr int SB = swap_rbit<LC>();
       uint32_t olane = lane;

@@ -185,6 +185,10 @@ __global__ void __launch_bounds__(THREADS)
     uint8_t *SH = shards + b * uint64_t(nv) * sstride;
     const uint8_t *P = payloads + b * pstride;
     S16 g0, g1;
+    // a wave none of whose 8 pieces exist (the payload's last, partial tile:
+    // 1 MB is 489 pieces, its 8th tile has 41) skips its transforms and only
+    // joins the barriers, the table DMAs and the row stores (uniform)
+    const bool idle = piece0 + 8 * wave >= npieces;
     const auto load_coef = [&]() __attribute__((always_inline)) {
       // opaque addresses: the values stored after the IFFT must be read back,
       // not forwarded from the registers (which would stay live meanwhile)
@@ -199,42 +203,48 @@ __global__ void __launch_bounds__(THREADS)
         g1.h[r] = y.y;
       }
     };
-    load_group(g0, P, plen, piece0 + 8 * wave, lane);
-    load_group(g1, P, plen, piece0 + 8 * wave + 4, lane);
+    if (!idle) {
+      load_group(g0, P, plen, piece0 + 8 * wave, lane);
+      load_group(g1, P, plen, piece0 + 8 * wave + 4, lane);
+    }
     // systematic shards 0..1023 = the data symbols (poly_encoder.hpp:239)
 #pragma unroll
     for (uint32_t hf = 0; hf < 2; ++hf) {
       lds_barrier();  // the other waves are done reading the regions
-      stage_half(g0, g1, my, lane, wave, hf);
+      if (!idle) stage_half(g0, g1, my, lane, wave, hf);
       lds_barrier();
       store_half(regions, SH, sstride, 512 * hf, nv, piece0, npieces, wave, lane);
     }
     // the index-0 tables (the last tile's DMA) landed; the regions are free
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
-    to_tower(g0, g1);
-    ifft1024<true, tower_sub_min(0)>(g0, tabs, my, lane);
-    ifft1024<true, tower_sub_min(0)>(g1, tabs, my, lane);
+    if (!idle) {
+      to_tower(g0, g1);
+      ifft1024<true, tower_sub_min(0)>(g0, tabs, my, lane);
+      ifft1024<true, tower_sub_min(0)>(g1, tabs, my, lane);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {  // read back by cosets 2 and 3 (coset 1 uses the registers)
-      cw0[r * 64 + lane] = make_uint2(g0.l[r], g0.h[r]);
-      cw1[r * 64 + lane] = make_uint2(g1.l[r], g1.h[r]);
+      for (int r = 0; r < 16; ++r) {  // read back by cosets 2 and 3 (coset 1 uses the registers)
+        cw0[r * 64 + lane] = make_uint2(g0.l[r], g0.h[r]);
+        cw1[r * 64 + lane] = make_uint2(g1.l[r], g1.h[r]);
+      }
     }
     lds_barrier();  // every wave is done with the index-0 tables
     Tabs::dma_image<THREADS>(tabs, t.timg_t + kTabImageBytes, tid);
     // cs: std::integral_constant coset number (its image's subfield stages)
     const auto coset = [&](auto cs) __attribute__((always_inline)) {
       constexpr uint32_t s = decltype(cs)::value;
-      if (s > 1) load_coef();
+      if (s > 1 && !idle) load_coef();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // coset s's tables and coefficients landed
       lds_barrier();  // (all waves' slices) and the regions are free
-      fft1024<false, tower_sub_min(int(s))>(g0, tabs, my, lane);
-      fft1024<false, tower_sub_min(int(s))>(g1, tabs, my, lane);
-      to_tower(g0, g1);  // back to symbol coordinates
+      if (!idle) {
+        fft1024<false, tower_sub_min(int(s))>(g0, tabs, my, lane);
+        fft1024<false, tower_sub_min(int(s))>(g1, tabs, my, lane);
+        to_tower(g0, g1);  // back to symbol coordinates
+      }
 #pragma unroll
       for (uint32_t hf = 0; hf < 2; ++hf) {
         if (hf) lds_barrier();
-        stage_half(g0, g1, my, lane, wave, hf);
+        if (!idle) stage_half(g0, g1, my, lane, wave, hf);
         lds_barrier();
         if (hf == 0)  // every wave is past its FFT: the next set (index 0 after the last coset)
           Tabs::dma_image<THREADS>(tabs, t.timg_t + (s + 1 < ncos ? s + 1 : 0) * kTabImageBytes, tid);
