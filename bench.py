@@ -214,14 +214,17 @@ def size_sweep(args, nv, cnt_key, dev, stream, dist, world, rank, backend, headl
                     e[3].record(stream)
                     ev.append(e)
 
-            for _ in range(args.warmup):
+            # sub-millisecond steps: more of them (launch latency and clock ramp
+            # dominate a handful), as many on every rank
+            steps = args.steps if plen >= args.payload else max(args.steps, 50)
+            for _ in range(args.warmup if plen >= args.payload else max(args.warmup, 5)):
                 step(False)
             torch.cuda.synchronize(dev)
             if dist:
                 dist.barrier()
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
-            for _ in range(args.steps):
+            for _ in range(steps):
                 step(True)
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
@@ -236,8 +239,9 @@ def size_sweep(args, nv, cnt_key, dev, stream, dist, world, rank, backend, headl
             dom = max(kern, key=lambda x: kern[x][0])
             achieved = kern[dom][1] / (kern[dom][0] * 1e-3)
             row = {"payload_bytes": plen, "batch_per_gpu": B,
-                   "ms_per_step": round(el / args.steps * 1e3, 4),
-                   "GiBps": round(world * B * plen * args.steps / el / 2**30, 3),
+                   "steps": steps,
+                   "ms_per_step": round(el / steps * 1e3, 4),
+                   "GiBps": round(world * B * plen * steps / el / 2**30, 3),
                    "kernels_ms": {"encode": round(t_enc, 4), "error_locator": round(t_loc, 4),
                                   "reconstruct": round(t_rec, 4)},
                    "roofline": {"kernel": dom, "achieved_GBps": round(achieved / 1e9, 2),

@@ -55,8 +55,10 @@ hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t 
 hipError_t launch_error_locator(const CodeParams &p, const uint8_t *d_present, size_t batch,
                                 const uint16_t *d_fold, const uint32_t *d_pattern,
                                 uint16_t *d_err_log, hipStream_t s);
-// Pattern dedup: d_pattern[b] = the smallest index whose
-// erasure pattern equals payload b's.  Needs dedup_scratch_bytes(batch).
+// Pattern dedup: d_pattern[b] = a row whose erasure
+// pattern equals payload b's and which is its own leader, or b itself (a hash
+// collision with a different pattern only costs the sharing; ec_amd.h).
+// Needs dedup_scratch_bytes(batch); batch < 2^31.
 // true if launch_error_locator runs the wave-per-pattern form (64 <= n <= 4096),
 // cheap enough that a batch computes every row instead of deduplicating
 bool locator_wave_applicable(uint32_t n);

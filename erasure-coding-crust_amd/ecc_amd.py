@@ -295,7 +295,8 @@ def reconstruct_batch(nv, d_shards, shard_len_, shard_stride, d_present, d_err_l
 
 
 def dedup_patterns(nv, d_present, batch, d_pattern, stream=None):
-    """d_pattern[b] (uint32) = smallest index with the same erasure pattern as b."""
+    """d_pattern[b] (uint32) = a row with the same erasure pattern as b that is its own
+    leader (d_pattern[l] == l), or b itself (ec_amd.h)."""
     _check(lib().ECCR_AMD_dedup_patterns(nv, _p(d_present), batch, _p(d_pattern), _stream(stream)),
            "dedup_patterns")
 
