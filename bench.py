@@ -166,6 +166,46 @@ def cpu_size_rate(nv, plen, cnt, seconds, threads):
             f"GiBps_{threads}threads": round(dn * plen / wn / 2**30, 6)}
 
 
+def device_bandwidth(dev, nbytes=1 << 30, reps=5):
+    """Measured device bandwidth on this box (the roofline also
+    against a measured copy): a 1 GiB device-to-device copy (read + write
+    bytes) and a 1 GiB fill (write bytes), HIP events on the current stream."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1)
+    b.copy_(a)
+    out = {}
+    for name, fn, moved in (("copy_GBps", lambda: b.copy_(a), 2 * nbytes),
+                            ("fill_GBps", lambda: b.fill_(7), nbytes)):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        out[name] = round(moved * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    del a, b
+    torch.cuda.empty_cache()
+    return out
+
+
+def gf_mul_counts(nv, n, k, cnt):
+    """GF(2^16) multiplies the reference algorithm executes (SURVEY.md §8d
+    secondary ceiling; additive_fft.hpp:99-141 skips the 0xFFFF skews, one
+    block per stage at index 0): encode per 2k-byte piece = inverse_afft(k) at
+    0 + (n/k - 1) afft(k) at the cosets (poly_encoder.hpp:217-240); reconstruct
+    per shard column = c locator products + inverse_afft(n) + afft(n) at 0 +
+    the erased outputs y < k (poly_encoder.hpp:164-189; k - present data rows
+    on average k (1 - c/nv))."""
+    lk, ln = k.bit_length() - 1, n.bit_length() - 1
+    ifft_k = k // 2 * lk - (k - 1)
+    enc = ifft_k + (n // k - 1) * (k // 2 * lk)
+    fft_n = n // 2 * ln - (n - 1)
+    rec = cnt + 2 * fft_n + k * (1 - cnt / nv)
+    return enc, rec
+
+
 def size_sweep(args, nv, cnt_key, dev, stream, dist, world, rank, backend, headline):
     """Device-resident encode + locator + reconstruct at each benchmark/ size
     (north_star): the same step as the headline on synthetic payloads of that
@@ -467,6 +507,9 @@ def main():
     achieved = b_dom / (t_dom * 1e-3)
 
     traffic, traffic_src = pmc_traffic(dom, nv, plen, cnt, B)
+    bw = device_bandwidth(dev)
+    mul_enc, mul_rec = gf_mul_counts(nv, n, k, cnt)
+    pieces, cols = -(-plen // (2 * k)), sl // 2
     total_bytes = world * B * plen * args.steps
     value = total_bytes / elapsed / 2**30
     line = {
@@ -486,7 +529,16 @@ def main():
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "bytes_per_launch": b_dom, "avg_launch_ms": round(t_dom, 4),
-                     "issue": sq_issue(dom, nv)},
+                     "issue": sq_issue(dom, nv),
+                     "measured": dict(bw, frac_of_copy=round(achieved / (bw["copy_GBps"] * 1e9), 4))},
+        # secondary ceiling: the reference algorithm's GF(2^16)
+        # multiplies per second, against the register-only multiply stream
+        "gf_mul": {"encode_per_s": round(B * pieces * mul_enc / (t_enc * 1e-3), -9),
+                   "reconstruct_per_s": round(B * cols * mul_rec / (t_rec * 1e-3), -9),
+                   "per_piece_encode": mul_enc, "per_column_reconstruct": round(mul_rec, 1),
+                   "ceiling_per_s": 6.0e12,
+                   "ceiling_source": "scripts/micro/mulrate.hip: general v_perm multiply-accumulate "
+                                     "butterflies, tables in registers, 4 waves/SIMD (DESIGN.md §6)"},
         "kernels_ms": {"encode": round(t_enc, 4), "error_locator": round(t_loc, 4),
                        "reconstruct": round(t_rec, 4)},
         "encode_GiBps": round(world * B * plen / (t_enc * 1e-3) / 2**30, 3),

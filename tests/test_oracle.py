@@ -152,3 +152,28 @@ def test_afft_roundtrip(oracle, size, index):
     rng = np.random.default_rng(size + index)
     x = rng.integers(0, 65536, size, dtype=np.uint16)
     assert (oracle.inverse_afft(oracle.afft(x, index), index) == x).all()
+
+
+@pytest.mark.parametrize("nv,cnt", [(1024, 342), (4096, 1366), (100, 34)])
+def test_bench_gf_mul_counts(oracle, nv, cnt):
+    """bench.py's secondary-ceiling multiply counts equal the
+    butterflies with a non-0xFFFF skew that the reference's transforms run
+    (additive_fft.hpp:99-141), counted here from the oracle's skew table."""
+    import bench
+    sk = oracle.table("skews")
+    n, k = 1 << (nv - 1).bit_length(), None
+    thr = (nv - 1) // 3 + 1
+    k = 1 << (thr.bit_length() - 1)
+
+    def muls(size, index):
+        c, d = 0, 1
+        while d < size:
+            c += sum(1 for j in range(0, size, 2 * d) if sk[j + d - 1 + index] != 65535) * d
+            d *= 2
+        return c
+
+    enc = muls(k, 0) + sum(muls(k, s) for s in range(k, n, k))
+    rec_fft = muls(n, 0)
+    e, r = bench.gf_mul_counts(nv, n, k, cnt)
+    assert e == enc
+    assert r == pytest.approx(cnt + 2 * rec_fft + k * (1 - cnt / nv))
