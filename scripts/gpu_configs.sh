@@ -3,7 +3,7 @@
 # n_validators sweep incl. 4096 (config 4 per GPU), exactly-k erasures.
 set -u
 O=gpurun_out/configs; mkdir -p $O
-run() { local name=$1; shift; echo "== $name"; timeout -k 10 300 python bench.py "$@" > $O/$name.json 2> $O/$name.err || { tail -5 $O/$name.err; exit 1; }; cat $O/$name.json; }
+run() { local name=$1; shift; echo "== $name"; timeout -k 10 300 python bench.py --sweep none "$@" > $O/$name.json 2> $O/$name.err || { tail -5 $O/$name.err; exit 1; }; cat $O/$name.json; }
 run c3_10MB_thr --payload 10000000 --batch 400 --steps 3 --warmup 1 --no-cpu-baseline
 run c3_10MB_k --payload 10000000 --batch 400 --present k --steps 3 --warmup 1 --no-cpu-baseline
 run c2_k --present k --steps 3 --warmup 1 --no-cpu-baseline
