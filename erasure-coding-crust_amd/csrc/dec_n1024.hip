@@ -124,6 +124,19 @@ __device__ __forceinline__ void tab_at(const uint8_t *, uint32_t lin, SubTab &T)
   lds_subtab_abs<Tabs::kPlane>(lin, T);
 }
 constexpr int SUB = tower_sub_min(0);
+// IFFT stage 1 with F9 tables (F9 image kind 0)
+#ifndef DEC_F9
+#define DEC_F9 1
+#endif
+constexpr bool kF9 = DEC_F9 != 0;
+__device__ __forceinline__ void tab_at(const uint8_t *, uint32_t lin, F9Tab &T) {
+  lds_f9tab_abs<Tabs::kPlane>(lin, T);
+}
+__device__ __forceinline__ void ib(S16 &s, int a, int b, const F9Tab &T) {
+  s.l[b] ^= s.l[a];
+  s.h[b] ^= s.h[a];
+  mul_acc_f9(s.l[b], s.h[b], T, s.l[a], s.h[a]);
+}
 
 // inverse radix-16 pass over position bits b0..b0+3: pos(r) = lane part | (r << b0),
 // lb = tlin(lane part).  15 tables (8 + 4 + 2 + 1), each requested one step
@@ -131,10 +144,12 @@ constexpr int SUB = tower_sub_min(0);
 template <int B0>
 __device__ __forceinline__ void ipass4(S16 &s, const uint8_t *tabs, uint32_t lb) {
   Tab T[2];      // stages < SUB: general tables
+  F9Tab F[2];    // stage 1 (kF9): F9 tables
   SubTab U[2];   // stages >= SUB: subfield tables
   const auto fetch = [&](int t, int blk, int slot) __attribute__((always_inline)) {
     const uint32_t a = lb ^ tlin(skew_idx(uint32_t(blk) << B0, B0 + t));
     if (B0 + t >= SUB) tab_at(tabs, a, U[slot]);
+    else if (kF9 && B0 + t == 1) tab_at(tabs, a, F[slot]);
     else tab_at(tabs, a, T[slot]);
   };
   fetch(0, 0, 0);
@@ -149,6 +164,7 @@ __device__ __forceinline__ void ipass4(S16 &s, const uint8_t *tabs, uint32_t lb)
 #pragma unroll
       for (int i = 0; i < d; ++i) {
         if (B0 + t >= SUB) ib(s, blk + i, blk + i + d, U[k & 1]);
+        else if (kF9 && B0 + t == 1) ib(s, blk + i, blk + i + d, F[k & 1]);
         else ib(s, blk + i, blk + i + d, T[k & 1]);
       }
     }
@@ -316,7 +332,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   // multiply tables for skew indices 0..1022: the prebuilt LDS image 0
   // (DevTables::timg), one coalesced 80 KB copy instead of a 1023-entry gather
   // through the skews (that gather was ~10 us of every launch; small calls pay it)
-  Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);
+  Tabs::copy_image<THREADS>(tabs, kF9 ? t.timg_f9 : t.timg_t, tid0);  // F9 kind 0
   __syncthreads();
 #ifdef DEC_STAMP
   uint64_t st_ = __builtin_amdgcn_s_memtime(), acc_[11] = {};

@@ -164,6 +164,47 @@ __device__ __forceinline__ void mul_acc_sub(uint32_t xl, uint32_t xh, const SubT
   yh = xor3(yh, vperm(T.t[1], T.t[0], s3), vperm(T.t[3], T.t[2], s4)) ^ vperm(T.t[4], T.t[4], s5);
 }
 
+// ---- F9 multiplies: a constant c0 + c1 w with c1 in {0, 1}
+// (tower coordinates, w^2 = alpha w + beta) as three subfield tables and a mask:
+//   low  ^= c0 x0 ^ (c1 beta) x1,   high ^= (c0 + c1 alpha) x1 ^ (x0 & m)
+// 9 v_perm + 6 v_and + 2 v_lshrrev_b64 + 5 XOR + 1 v_and = 32 issue slots per
+// 4 multiply-accumulates (mul_acc: 38).  F9Tab = MulTabF9 (gf_field.hpp).
+struct F9Tab {
+  uint32_t t[16];
+};
+
+__device__ __forceinline__ void mul_acc_f9(uint32_t xl, uint32_t xh, const F9Tab &T, uint32_t &yl,
+                                           uint32_t &yh) {
+  const uint64_t x = (uint64_t(xh) << 32) | xl;
+  const uint64_t t3 = shr64<3>(x), t6 = shr64<6>(x);
+  const uint32_t s0 = xl & 0x07070707u;
+  const uint32_t s1 = uint32_t(t3) & 0x07070707u;
+  const uint32_t s2 = uint32_t(t6) & 0x03030303u;
+  const uint32_t s3 = xh & 0x07070707u;
+  const uint32_t s4 = uint32_t(t3 >> 32) & 0x07070707u;
+  const uint32_t s5 = uint32_t(t6 >> 32) & 0x03030303u;
+  uint32_t l = xor3(yl, vperm(T.t[1], T.t[0], s0), vperm(T.t[3], T.t[2], s1));
+  l = xor3(l, vperm(T.t[4], T.t[4], s2), vperm(T.t[6], T.t[5], s3));
+  yl = xor3(l, vperm(T.t[8], T.t[7], s4), vperm(T.t[9], T.t[9], s5));
+  const uint32_t h = xor3(yh, vperm(T.t[11], T.t[10], s3), vperm(T.t[13], T.t[12], s4));
+  yh = xor3(h, vperm(T.t[14], T.t[14], s5), xl & T.t[15]);
+}
+
+// An F9 table in an F9 image slot at absolute LDS address `a` (plane 0;
+// planes PLANE bytes apart): planes 0..3
+template <int PLANE>
+__device__ __forceinline__ void lds_f9tab_abs(uint32_t a, F9Tab &T) {
+#pragma unroll
+  for (int q = 3; q >= 0; --q) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u v = *(const __attribute__((address_space(3))) v4u *)(uintptr_t(a + q * PLANE));
+    T.t[4 * q] = v.x;
+    T.t[4 * q + 1] = v.y;
+    T.t[4 * q + 2] = v.z;
+    T.t[4 * q + 3] = v.w;
+  }
+}
+
 // symbol <-> tower coordinates of a byte-planar group (the map is its own
 // inverse): l ^= L(h) bytewise, L = kTowerL, as compile-time v_perm tables
 __host__ __device__ constexpr uint8_t tower_l8(uint32_t h) {

@@ -24,6 +24,17 @@ constexpr int kTabImages = 4;
 // below; a kernel reading set q uses mul_acc_sub at exactly those stages.
 constexpr int tower_sub_min(int q) { return q == 0 ? 2 : q == 1 ? 3 : 4; }
 
+// F9 variants of tower image 0: entry i holds a MulTabF9
+// (plane q = w[4q .. 4q + 3]) where f9_slot(kind, i), the tower image's table
+// elsewhere.  Kind 0 (reconstruct_n1024): the stage-1 entries (i = 1 mod 4,
+// elements 0..510); kind 1 (encode_k256): also the stage-0 entries
+// 256..510 (elements 256..510, its coset-256 FFT).  Their elements' high
+// tower coordinate is 0 or 1 (tests/cpp/tower_check.cpp).
+constexpr int kF9Images = 2;
+constexpr bool f9_slot(int kind, uint32_t i) {
+  return i % 4 == 1 || (kind == 1 && i % 2 == 0 && i >= 256 && i < 512);
+}
+
 struct DevTables {
   const uint16_t *skews = nullptr;     // 65535
   const MulTab *mtab = nullptr;        // 65536
@@ -31,6 +42,7 @@ struct DevTables {
   const MulTab *mtab_tin = nullptr;    // 65536, symbols in, tower out
   const MulTab *mtab_tout = nullptr;   // 65536, tower in, symbols out
   const uint8_t *timg_t = nullptr;     // kTabImages x kTabImageBytes, tower images
+  const uint8_t *timg_f9 = nullptr;    // kF9Images x kTabImageBytes, F9 variants of tower image 0
 };
 
 // Per (device, kernel), once and thread-safe: raise `fn`'s dynamic-LDS limit

@@ -21,6 +21,7 @@ struct DeviceState {
   uint8_t *timg = nullptr;
   MulTab *mtab_t = nullptr;  // mtab_tin, then mtab_tout
   uint8_t *timg_t = nullptr;
+  uint8_t *timg_f9 = nullptr;
   std::mutex mu;
   std::map<uint32_t, uint16_t *> fold;
   std::mutex scratch_mu;  // held by a ScratchLease
@@ -104,6 +105,23 @@ DeviceState *device_state() {
           std::memcpy(&img_t[slot + plane * 16384], reinterpret_cast<const uint8_t *>(&g) + 16 * plane, 16);
       }
     }
+  std::vector<uint8_t> img_f9(kF9Images * kTabImageBytes, 0);
+  for (int kind = 0; kind < kF9Images; ++kind) {
+    std::memcpy(&img_f9[size_t(kind) * kTabImageBytes], img_t.data(), kTabImageBytes);
+    for (uint32_t i = 0; i < 1023; ++i) {
+      if (!f9_slot(kind, i)) continue;
+      MulTabF9 t9;
+      if (!f.f9_tab(f.skews[i], &t9)) return nullptr;  // (tower_check: never)
+      const uint32_t sw = (i ^ (i >> 4) ^ (i >> 8)) & 15;
+      const size_t slot = size_t(kind) * kTabImageBytes + ((i >> 4) << 8) + (sw << 4);
+      for (uint32_t plane = 0; plane < 4; ++plane)
+        std::memcpy(&img_f9[slot + plane * 16384], &t9.w[4 * plane], 16);
+    }
+  }
+  if (!hip_ok(hipMalloc(&st->timg_f9, img_f9.size()), "hipMalloc(F9 images)") ||
+      !hip_ok(hipMemcpy(st->timg_f9, img_f9.data(), img_f9.size(), hipMemcpyHostToDevice),
+              "upload F9 images"))
+    return nullptr;
   if (!hip_ok(hipMalloc(&st->timg, img.size()), "hipMalloc(table images)") ||
       !hip_ok(hipMemcpy(st->timg, img.data(), img.size(), hipMemcpyHostToDevice),
               "upload table images") ||
@@ -139,6 +157,7 @@ DevTables device_tables(DeviceState *d) {
   t.mtab_tin = d->mtab_t;
   t.mtab_tout = d->mtab_t + kFieldSize;
   t.timg_t = d->timg_t;
+  t.timg_f9 = d->timg_f9;
   return t;
 }
 

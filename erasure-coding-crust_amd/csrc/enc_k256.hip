@@ -88,6 +88,24 @@ struct TabSel<true> {
 };
 template <int M, int SM>
 using TabAt = typename TabSel<(M >= SM)>::type;
+// F9 tables (F9 image kind 1) where F is set
+template <int M, int SM, bool F>
+using TabAtF = std::conditional_t<F, F9Tab, TabAt<M, SM>>;
+#ifndef ENC_F9
+#define ENC_F9 1
+#endif
+constexpr bool kF9 = ENC_F9 != 0;
+
+__device__ __forceinline__ void lds_tab_at(const uint8_t *lds, uint32_t lin, F9Tab &T) {
+#pragma unroll
+  for (int q = 3; q >= 0; --q) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(lds + q * Tabs::kPlane + lin);
+    T.t[4 * q] = v.x;
+    T.t[4 * q + 1] = v.y;
+    T.t[4 * q + 2] = v.z;
+    T.t[4 * q + 3] = v.w;
+  }
+}
 
 __device__ __forceinline__ void mul_any(uint32_t xl, uint32_t xh, const Tab &T, uint32_t &yl, uint32_t &yh) {
   mul_acc(xl, xh, T, yl, yh);
@@ -95,6 +113,10 @@ __device__ __forceinline__ void mul_any(uint32_t xl, uint32_t xh, const Tab &T, 
 __device__ __forceinline__ void mul_any(uint32_t xl, uint32_t xh, const SubTab &T, uint32_t &yl,
                                         uint32_t &yh) {
   mul_acc_sub(xl, xh, T, yl, yh);
+}
+__device__ __forceinline__ void mul_any(uint32_t xl, uint32_t xh, const F9Tab &T, uint32_t &yl,
+                                        uint32_t &yh) {
+  mul_acc_f9(xl, xh, T, yl, yh);
 }
 
 // skew index of the block holding position pos_a at stage m (additive_fft.hpp:108,126)
@@ -180,12 +202,12 @@ __device__ __forceinline__ void ipass3(State &s, const uint8_t *tabs, uint32_t b
   }
 }
 
-// forward: stages b0+2, b0+1, b0
-template <int b0, int SM, int SL = SM>
+// forward: stages b0+2, b0+1, b0 (F0 / F1: stage b0 / b0 + 1 with F9 tables)
+template <int b0, int SM, int SL = SM, bool F0 = false, bool F1 = false>
 __device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t base, uint32_t off) {
   {
-    TabAt<b0, SL> Ta0, Tb0;
-    TabAt<b0 + 1, SL> Ta1, Tb1;
+    TabAtF<b0, SL, F0> Ta0, Tb0;
+    TabAtF<b0 + 1, SL, F1> Ta1, Tb1;
     TabAt<b0 + 2, SL> Ta2;
     const PassIdx<b0, SM, SL> ix(base, off);
     const auto i0 = [&](int rr) { return ix.i0(rr); };
@@ -517,12 +539,14 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
   // (DevTables::timg), one coalesced 80 KB copy instead of a 1023-entry gather
   // through the skews (that gather was ~10 us of every launch; small calls pay it)
   // the tower images: the transforms run in tower coordinates
-  Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);
+  // (image 0 as its F9 variant kind 1: DESIGN.md §2.8)
+  const uint8_t *const img0 = kF9 ? t.timg_f9 + kTabImageBytes : t.timg_t;
+  Tabs::copy_image<THREADS>(tabs, img0, tid0);
   __syncthreads();
   [[maybe_unused]] int img = 0;
   [[maybe_unused]] const auto load_image = [&](int q) {  // LDS-DMA: no VGPRs (the kernel is at 128)
     lds_barrier();  // every wave is done with the current tables
-    Tabs::dma_image<THREADS>(tabs, t.timg_t + q * kTabImageBytes, tid0);
+    Tabs::dma_image<THREADS>(tabs, q == 0 ? img0 : t.timg_t + q * kTabImageBytes, tid0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
   };
@@ -703,8 +727,11 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     // ---- FFT_256 at each coset shift (encodeLow, poly_encoder.hpp:229-237)
     // sm: the tower image's first subfield stage (std::integral_constant)
     // sl: first subfield stage of this coset's pass A (<= SM: aliased stages)
-    const auto coset = [&](auto sm, auto sl, const uint32_t sh, const uint32_t off) __attribute__((always_inline)) {
+    // f0 / f1: pass A's stage 0 / 1 with F9 tables (std::integral_constant)
+    const auto coset = [&](auto sm, auto sl, auto f0, auto f1, const uint32_t sh, const uint32_t off)
+                           __attribute__((always_inline)) {
       constexpr int SM = decltype(sm)::value, SL = decltype(sl)::value;
+      constexpr bool F0 = decltype(f0)::value, F1 = decltype(f1)::value;
       s = coef;
       // opaque copy: keeps the compiler from hoisting the first stage's selector
       // masks out of the coset loop (that costs ~50 VGPRs and forces spills)
@@ -717,7 +744,7 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
       exchange<LC, LB>(s, xch, xb);
       fpass3<3, SM>(s, tabs, posB(q, 0), off);
       exchange<LB, LA>(s, xch, xb);
-      fpass3<0, SM, SL>(s, tabs, posA(q, 0), off);
+      fpass3<0, SM, SL, F0, F1>(s, tabs, posA(q, 0), off);
       {  // back to symbol coordinates
         const TowerK tk = tower_k();
 #pragma unroll
@@ -730,16 +757,20 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     };
     using Sub0 = std::integral_constant<int, tower_sub_min(0)>;
     using Sub1 = std::integral_constant<int, tower_sub_min(1)>;
-    // coset 1 (index 256): stage 1 skews are 128 + 2 (pos >> 2), subfield
-    coset(Sub0(), std::integral_constant<int, 1>(), K, K);  // (nv > 256 for k = 256)
-    for (uint32_t sh = 2 * K; sh < 1024u && int(sh) < nv; sh += K) coset(Sub0(), Sub0(), sh, sh);
+    using F9on = std::integral_constant<bool, kF9>;
+    using F9off = std::integral_constant<bool, false>;
+    // coset 1 (index 256): stage 1 skews are 128 + 2 (pos >> 2), subfield;
+    // stage 0's elements 256..510 take F9 tables
+    coset(Sub0(), std::integral_constant<int, 1>(), F9on(), F9off(), K, K);  // (nv > 256 for k = 256)
+    // cosets 2, 3: stage 1's elements 256..510 take F9 tables
+    for (uint32_t sh = 2 * K; sh < 1024u && int(sh) < nv; sh += K) coset(Sub0(), Sub0(), F9off(), F9on(), sh, sh);
     if constexpr (N > 1024) {
       for (uint32_t sh = 1024u; sh < uint32_t(N) && int(sh) < nv; sh += K) {
         if (sh == 1024u) {
           load_image(1);
           img = 1;
         }
-        coset(Sub1(), Sub1(), sh, sh & 1023u);
+        coset(Sub1(), Sub1(), F9off(), F9off(), sh, sh & 1023u);
       }
     }
   }

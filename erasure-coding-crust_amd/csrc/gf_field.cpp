@@ -139,6 +139,22 @@ MulTabSub Field::sub_tab(uint32_t c) const {
   return t;
 }
 
+bool Field::f9_tab(uint32_t c, MulTabF9 *t) const {
+  const uint16_t e = c == kZeroTab ? uint16_t(0) : exp[c];
+  const uint16_t te = tower(e), w2 = tower(mul(0x100, log[0x100]));  // tower(0x100) = 0x100
+  const uint32_t c0 = te & 0xff, c1 = te >> 8, beta = w2 & 0xff, alpha = w2 >> 8;
+  if (c1 > 1) return false;
+  const auto lg = [&](uint32_t v) { return v == 0 ? kZeroTab : uint32_t(log[v]); };
+  const MulTabSub a = sub_tab(lg(c0)), b = sub_tab(lg(c1 ? beta : 0)), d = sub_tab(lg(c0 ^ (c1 ? alpha : 0)));
+  for (int i = 0; i < 5; ++i) {
+    t->w[i] = a.w[i];
+    t->w[5 + i] = b.w[i];
+    t->w[10 + i] = d.w[i];
+  }
+  t->w[15] = c1 ? 0xffffffffu : 0u;
+  return true;
+}
+
 std::vector<uint16_t> Field::fold_log_walsh(uint32_t n) const {
   std::vector<uint16_t> F(n);
   for (uint32_t lo = 0; lo < n; ++lo) {

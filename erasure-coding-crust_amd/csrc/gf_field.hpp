@@ -57,6 +57,16 @@ struct MulTabSub {
   uint32_t w[5];
 };
 
+// "F9" table of a constant g^c whose tower coordinates are c0 + c1 w with
+// c1 in {0, 1}: with w^2 = alpha w + beta,
+//   (x0 + x1 w)(c0 + c1 w) = (c0 x0 + c1 beta x1) + ((c0 + c1 alpha) x1 + c1 x0) w,
+// three subfield tables and a mask (9 v_perm instead of 12):
+// w[0..4] = sub table of c0, w[5..9] = of c1 beta, w[10..14] = of c0 + c1 alpha,
+// w[15] = c1 ? ~0 : 0.  In a tower image slot: plane q holds w[4q .. 4q + 3].
+struct MulTabF9 {
+  uint32_t w[16];
+};
+
 struct Field {
   std::vector<uint16_t> log, exp, log_walsh;  // 65536 each (f2e16.hpp:48-84)
   std::vector<uint16_t> skews;                // 65535 (additive_fft.hpp:47-97)
@@ -70,6 +80,8 @@ struct Field {
   // general table of x -> T(T(x) * g^c) (tower in and out)
   MulTab tower_tab(uint32_t c) const;
   MulTabSub sub_tab(uint32_t c) const;  // requires g^c < 256 (or c = 65535)
+  // requires (tower(g^c) >> 8) <= 1; returns false (and leaves t) otherwise
+  bool f9_tab(uint32_t c, MulTabF9 *t) const;
 
   uint16_t mul(uint16_t x, uint32_t log_c) const {
     if (x == 0) return 0;

@@ -1,7 +1,8 @@
 // tower_check.cpp — CPU check of the tower-coordinate multiply tables
 // (gf_field.hpp), built by tests/test_tower.py with g++ against
 // erasure-coding-crust_amd/csrc/gf_field.cpp.  Emulates the device multiply
-// forms (mul_acc: 12 v_perm, mul_acc_sub: 6 v_perm, ec_device.hpp) byte for
+// forms (mul_acc: 12 v_perm, mul_acc_sub: 6 v_perm, mul_acc_f9: 9 v_perm,
+// ec_device.hpp) byte for
 // byte and checks every table kind against the field, and runs the additive
 // FFT / IFFT (additive_fft.hpp:99-141) in tower coordinates with the tower
 // image rule (ec_kernels.hpp tower_sub_min) against the plain transform.
@@ -55,6 +56,18 @@ static void mul_acc_sub(uint32_t xl, uint32_t xh, const MulTabSub &T, uint32_t &
   yh ^= vperm(w[1], w[0], s3) ^ vperm(w[3], w[2], s4) ^ vperm(w[4], w[4], s5);
 }
 
+// F9 form (ec_device.hpp mul_acc_f9): low ^= c0 x0 ^ c1 beta x1,
+// high ^= (c0 + c1 alpha) x1 ^ (x0 & m)
+static void mul_acc_f9(uint32_t xl, uint32_t xh, const MulTabF9 &T, uint32_t &yl, uint32_t &yh) {
+  const uint64_t x = (uint64_t(xh) << 32) | xl, t3 = x >> 3, t6 = x >> 6;
+  const uint32_t s0 = xl & 0x07070707u, s1 = uint32_t(t3) & 0x07070707u, s2 = uint32_t(t6) & 0x03030303u;
+  const uint32_t s3 = xh & 0x07070707u, s4 = uint32_t(t3 >> 32) & 0x07070707u, s5 = uint32_t(t6 >> 32) & 0x03030303u;
+  const uint32_t *w = T.w;
+  yl ^= vperm(w[1], w[0], s0) ^ vperm(w[3], w[2], s1) ^ vperm(w[4], w[4], s2) ^ vperm(w[6], w[5], s3) ^
+        vperm(w[8], w[7], s4) ^ vperm(w[9], w[9], s5);
+  yh ^= vperm(w[11], w[10], s3) ^ vperm(w[13], w[12], s4) ^ vperm(w[14], w[14], s5) ^ (xl & w[15]);
+}
+
 // one symbol through a multiply form (lane 0 of a byte-planar group)
 template <typename T, typename M>
 static uint16_t apply(M m, const T &tab, uint16_t x) {
@@ -94,6 +107,29 @@ int main() {
       CHECK(apply(mul_acc_sub, st, f.tower(x)) == f.tower(p), "sub e=%u x=%u", e, x);
     }
   }
+  // F9 tables: every constant whose high tower coordinate is 0 or 1
+  int nf9 = 0;
+  for (uint32_t e = 0; e < kFieldSize; e += (e < 1024 ? 1 : 61)) {  // by element value
+    const uint32_t cl = e == 0 ? kZeroTab : f.log[e];
+    MulTabF9 t9;
+    const bool ok = f.f9_tab(cl, &t9);
+    CHECK(ok == ((f.tower(uint16_t(e)) >> 8) <= 1), "f9 domain e=%u", e);
+    if (!ok) continue;
+    ++nf9;
+    for (int it = 0; it < 16; ++it) {
+      const uint16_t x = uint16_t(rng());
+      const uint16_t p = cl == kZeroTab ? 0 : f.mul(x, cl);
+      CHECK(apply(mul_acc_f9, t9, f.tower(x)) == f.tower(p), "f9 c=%u x=%u", cl, x);
+    }
+  }
+  CHECK(nf9 >= 512, "f9 constants %d", nf9);
+  // the F9 image rule (ec_kernels.hpp f9_slot): image 0's stage-1 entries
+  // (i = 1 mod 4) and, in the encode's image, its stage-0 entries 256..510
+  // have high tower coordinate <= 1
+  for (uint32_t i = 0; i < 1023; ++i) {
+    MulTabF9 t9;
+    if (i % 4 == 1 || (i % 2 == 0 && i >= 256 && i < 512)) CHECK(f.f9_tab(f.skews[i], &t9), "f9 slot %u", i);
+  }
   // the tower image rule: every entry at a stage >= tower_sub_min(q) is a
   // subfield skew (ec_kernels.hpp; mirrored here)
   const auto sub_min = [](int q) { return q == 0 ? 2 : q == 1 ? 3 : 4; };
@@ -128,14 +164,18 @@ int main() {
         a[i] = uint16_t(rng());
         t[i] = f.tower(a[i]);
       }
-      const auto mulp = [&](uint16_t x, uint32_t skew_i, bool tower) -> uint16_t {
-        const uint32_t c = f.skews[skew_i];
+      std::vector<uint16_t> t9 = t;  // tower coordinates, F9 tables at the encode image's F9 slots
+      const auto mulp = [&](uint16_t x, uint32_t skew_i, int tower) -> uint16_t {
+        const uint32_t c = f.skews[skew_i], i = skew_i - index;
         if (!tower) return apply(mul_acc, f.mtab[c], x);
         if (__builtin_ctz(skew_i + 1) >= sub_min(q)) return apply(mul_acc_sub, f.sub_tab(c), x);
+        MulTabF9 tf;
+        if (tower == 2 && q == 0 && (i % 4 == 1 || (i % 2 == 0 && i >= 256 && i < 512)) && f.f9_tab(c, &tf))
+          return apply(mul_acc_f9, tf, x);
         return apply(mul_acc, f.tower_tab(c), x);
       };
-      for (int tw = 0; tw < 2; ++tw) {
-        std::vector<uint16_t> &d = tw ? t : a;
+      for (int tw = 0; tw < 3; ++tw) {
+        std::vector<uint16_t> &d = tw == 2 ? t9 : tw ? t : a;
         if (inverse) {
           for (uint32_t dep = 1; dep < n; dep <<= 1)
             for (uint32_t j = dep; j < n; j += 2 * dep) {
@@ -151,6 +191,7 @@ int main() {
         }
       }
       for (uint32_t i = 0; i < n; ++i) CHECK(f.tower(t[i]) == a[i], "fft q=%d inv=%d i=%u", q, inverse, i);
+      for (uint32_t i = 0; i < n; ++i) CHECK(t9[i] == t[i], "f9 fft q=%d inv=%d i=%u", q, inverse, i);
     }
   if (fails) {
     std::printf("%d failures\n", fails);
