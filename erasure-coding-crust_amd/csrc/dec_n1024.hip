@@ -361,8 +361,10 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   // m[2], m[3]: the output rows y = 4 lane + q (q = 0..3) of phase 5, 16 bits
   // each: 0xFFFF = present (copied from the staged row), else mul_index(E[y]) (the
   // erased value is scaled by E[y]; y < 256 < nv always holds for n = 1024).
-  auto load_meta = [&](uint64_t tl, uint32_t tid, uint32_t (&m)[4]) {
-    const uint64_t bb = PACKED ? uint64_t(uint32_t(tl) / gpp) : tl / tiles_pp;
+  TileWalk walk(first, step, tiles_pp);  // !PACKED: payload and tile of `tile`
+  // bb: the payload of tile tl (!PACKED: from the walk, no division)
+  auto load_meta = [&](uint64_t tl, uint64_t bw, uint32_t tid, uint32_t (&m)[4]) {
+    const uint64_t bb = PACKED ? uint64_t(uint32_t(tl) / gpp) : bw;
     const uint64_t pt = pattern ? pattern[bb] : bb;
     if constexpr (!PACKED) {
 #pragma unroll
@@ -380,8 +382,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     }
   };
   uint32_t meta[4] = {0, 0, 0, 0}, meta_next[4] = {0, 0, 0, 0};
-  if (first < total) load_meta(first, tid0, meta);
-  for (uint64_t tile = first; tile < total; tile += step) {
+  if (first < total) load_meta(first, walk.b, tid0, meta);
+  for (uint64_t tile = first; tile < total; tile += step, walk.advance()) {
     // lane-derived addresses are recomputed per tile from an opaque copy of
     // the thread id (hoisted out of the loop they were kept live, and spilled,
     // across the whole tile)
@@ -393,8 +395,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       b = uint32_t(tile) / gpp;  // < 2^32 groups (launch check)
       col0 = 4 * uint64_t(uint32_t(tile) % gpp) - 4 * uint64_t(wave_s);  // cbase below = col0 + 4 * wave (mod 2^64)
     } else {
-      b = tile / tiles_pp;
-      col0 = (tile % tiles_pp) * COLS;
+      b = walk.b;
+      col0 = walk.i * COLS;
     }
     const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
     uint8_t *O = out + b * ostride;
@@ -543,7 +545,11 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
 #endif
     }
     }
-    if (tile + step < total) load_meta(tile + step, tid, meta_next);
+    if (tile + step < total) {
+      uint64_t nb, ni;
+      walk.next_of(nb, ni);
+      load_meta(tile + step, nb, tid, meta_next);
+    }
     STAMP(2);
     if constexpr (!PACKED) __syncthreads();  // packed: the wave's own region and staging only
     STAMP(3);

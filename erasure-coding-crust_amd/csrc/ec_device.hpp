@@ -71,6 +71,28 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// (payload, tile in payload) of a grid-stride tile walk, tile = b * per + i,
+// advanced by `step` tiles with an add and a compare instead of a 64-bit
+// division per tile (wave-uniform: SGPRs)
+struct TileWalk {
+  uint64_t b = 0, i = 0, qs = 0, rs = 0, per = 1;
+  __device__ TileWalk(uint64_t first, uint64_t step, uint64_t per_) : per(per_ ? per_ : 1) {
+    b = first / per;
+    i = first % per;
+    qs = step / per;
+    rs = step % per;
+  }
+  __device__ __forceinline__ void next_of(uint64_t &nb, uint64_t &ni) const {
+    ni = i + rs;
+    nb = b + qs;
+    if (ni >= per) {
+      ni -= per;
+      ++nb;
+    }
+  }
+  __device__ __forceinline__ void advance() { next_of(b, i); }
+};
+
 struct Tab {
   uint32_t t[20];
 };

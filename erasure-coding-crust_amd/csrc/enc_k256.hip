@@ -574,7 +574,8 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
       lds_barrier();
     }
   };
-  for (uint64_t tile = first; tile < total; tile += step) {
+  TileWalk walk(first, step, tiles_pp);  // PK = 0: payload and tile of `tile`
+  for (uint64_t tile = first; tile < total; tile += step, walk.advance()) {
     // lane ids made opaque per tile: per-lane LDS addresses are recomputed in the
     // loop instead of being hoisted out of it and spilled
     uint32_t tid = tid0;
@@ -597,8 +598,8 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
       b = bw;
       piece0 = pw;
     } else {
-      b = tile / tiles_pp;
-      piece0 = (tile % tiles_pp) * TILE;
+      b = walk.b;
+      piece0 = walk.i * TILE;
     }
     const uint8_t *P = payloads + b * pstride;
     uint8_t *SH = PACKED ? shards : shards + b * uint64_t(nv) * sstride;  // packed: per chunk
