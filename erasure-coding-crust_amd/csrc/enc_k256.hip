@@ -259,14 +259,25 @@ __device__ __forceinline__ void ipassC0(State &s, const uint8_t *tabs) {
   bxor(s, 5, 7);
 }
 
-__device__ __forceinline__ void fpassC(State &s, const uint8_t *tabs, uint32_t off) {
+// stage-7 butterfly reading the IFFT coefficients c and writing s (stage 7
+// touches every register, so the coset needs no copy of c)
+template <typename T>
+__device__ __forceinline__ void fbfly_from(State &s, const State &c, int ra, int rb, const T &Tb) {
+  s.l[0][ra] = c.l[0][ra];
+  s.h[0][ra] = c.h[0][ra];
+  mul_any(c.l[0][rb], c.h[0][rb], Tb, s.l[0][ra], s.h[0][ra]);
+  s.l[0][rb] = c.l[0][rb] ^ s.l[0][ra];
+  s.h[0][rb] = c.h[0][rb] ^ s.h[0][ra];
+}
+
+__device__ __forceinline__ void fpassC(State &s, const State &c, const uint8_t *tabs, uint32_t off) {
   SubTab Ta, Tb;  // stages 7, 6 >= tower_sub_min(0), tower_sub_min(1)
   lds_tab_at(tabs, tlin(skew_idx(0, 7, off)), Ta);
   lds_tab_at(tabs, tlin(skew_idx(0, 6, off)), Tb);
-  fbfly(s, 0, 2, Ta);
-  fbfly(s, 1, 3, Ta);
-  fbfly(s, 4, 6, Ta);
-  fbfly(s, 5, 7, Ta);
+  fbfly_from(s, c, 0, 2, Ta);
+  fbfly_from(s, c, 1, 3, Ta);
+  fbfly_from(s, c, 4, 6, Ta);
+  fbfly_from(s, c, 5, 7, Ta);
   lds_tab_at(tabs, tlin(skew_idx(1u << 7, 6, off)), Ta);
   fbfly(s, 0, 1, Tb);
   fbfly(s, 4, 5, Tb);
@@ -723,7 +734,7 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     ipass3<3, tower_sub_min(0)>(s, tabs, posB(q, 0), 0);
     exchange<LB, LC>(s, xch, xb);
     ipassC0(s, tabs);
-    const State coef = s;
+    State coef = s;
 
     // ---- FFT_256 at each coset shift (encodeLow, poly_encoder.hpp:229-237)
     // sm: the tower image's first subfield stage (std::integral_constant)
@@ -733,14 +744,12 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
                            __attribute__((always_inline)) {
       constexpr int SM = decltype(sm)::value, SL = decltype(sl)::value;
       constexpr bool F0 = decltype(f0)::value, F1 = decltype(f1)::value;
-      s = coef;
-      // opaque copy: keeps the compiler from hoisting the first stage's selector
-      // masks out of the coset loop (that costs ~50 VGPRs and forces spills)
+      // coef made opaque in place (no copy): keeps the compiler from hoisting
+      // the first stage's selector masks out of the coset loop (that costs ~50
+      // VGPRs and forces spills); pass C's stage 7 reads it and writes s
 #pragma unroll
-      for (int g = 0; g < GP; ++g)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(s.l[g][r]), "+v"(s.h[g][r]));
-      fpassC(s, tabs, off);
+      for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(coef.l[0][r]), "+v"(coef.h[0][r]));
+      fpassC(s, coef, tabs, off);
       rsync();  // previous coset's rows read out
       exchange<LC, LB>(s, xch, xb);
       fpass3<3, SM>(s, tabs, posB(q, 0), off);
