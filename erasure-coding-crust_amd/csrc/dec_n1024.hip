@@ -556,7 +556,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     const uint64_t cbase = col0 + 4 * wave;
     if constexpr (!PACKED) {
       // a group past the payload's last column (its last, partial tile: 1 MB
-      // shards are 977 columns, the 31st tile has 17): phases 2-5 are this
+      // shards are 1954 columns, the 62nd tile has 2): phases 2-5 are this
       // wave's alone, so it goes straight to the next tile's barrier
       if (col0 + 4 * uint64_t(wave_s) >= ncols) {
 #pragma unroll

@@ -628,7 +628,7 @@ __global__ void __launch_bounds__(THREADS) encode_k256(const uint8_t *__restrict
     };
 
     // A wave none of whose 8 pieces exist (the last, partial tile of a payload:
-    // 1 MB is 1953 pieces, its 16th tile has 33) skips the transforms and only
+    // 1 MB is 1954 pieces, its 16th tile has 34) skips the transforms and only
     // takes part in the barriers, the image loads and the row stores of the
     // others, in the same order as below (wave-uniform branch)
     if constexpr (PK == 0) {
