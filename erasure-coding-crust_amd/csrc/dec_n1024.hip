@@ -589,7 +589,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         s.l[r] = x.x;
         s.h[r] = x.y;
       }
-      prio_lead(wave & 4);
+      prio_lead(wave_s & 4);
       ipass4<0>(s, tabs, tlin(16 * lane));
 #pragma unroll
       for (int r = 0; r < 16; ++r) lds_st2(la ^ raddr(r), make_uint2(s.l[r], s.h[r]));
@@ -605,7 +605,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
         s.l[r] = x.x;
         s.h[r] = x.y;
       }
-      prio_lead(!(wave & 4));
+      prio_lead(!(wave_s & 4));
       ipass4<4>(s, tabs, tlin((lane >> 4) << 8));
 #pragma unroll
       for (int r = 0; r < 16; ++r) lds_st2(lb ^ raddr(uint32_t(r) << 4), make_uint2(s.l[r], s.h[r]));
@@ -641,7 +641,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       }
     }
 
-    prio_lead(wave & 4);
+    prio_lead(wave_s & 4);
     STAMP(4);
     // ---- phases 3 + 4a: formal derivative (poly_encoder.hpp:195-215) and FFT
     // stages 9, 8 (afft, additive_fft.hpp:121-141) for the outputs y < 256 only.
