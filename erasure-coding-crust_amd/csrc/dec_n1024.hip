@@ -553,7 +553,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     STAMP(2);
     if constexpr (!PACKED) __syncthreads();  // packed: the wave's own region and staging only
     STAMP(3);
-    const uint64_t cbase = col0 + 4 * wave;
+    const uint64_t cbase = col0 + 4 * uint64_t(wave_s);  // wave-uniform: phase 5's column tests stay scalar
     if constexpr (!PACKED) {
       // a group past the payload's last column (its last, partial tile: 1 MB
       // shards are 1954 columns, the 62nd tile has 2): phases 2-5 are this
