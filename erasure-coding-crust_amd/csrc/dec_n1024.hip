@@ -241,7 +241,8 @@ __device__ __forceinline__ uint2 load8_any(const uint8_t *p, uint32_t avail) {
 }
 
 // The two waves of a SIMD (w, w + 4) take turns at the higher issue priority
-// (pass A: w + 4, pass B: w, pass C to the FFT: w + 4, output: equal), so
+// (pass A: w + 4, pass B: w, pass C to the FFT: w + 4, output: w, gather:
+// equal), so
 // neither runs far ahead and then idles at the tile barrier while the other
 // finishes alone (the arbiter otherwise favours the older wave throughout).
 // A/B at B = 2048: 7.06 -> 7.01 ms; one fixed priority for the whole
@@ -780,7 +781,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       fb(0, 1, T[0]);  // stage 0
       fb(2, 3, T[1]);
     }
-    __builtin_amdgcn_s_setprio(0);
+    prio_lead(!(wave_s & 4));  // the output: w leads (11.26 -> 11.19 ms at B = 4096)
     STAMP(8);
     STAMP(9);
 
@@ -827,6 +828,11 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
     STAMP(10);
 #pragma unroll
     for (int i = 0; i < 4; ++i) meta[i] = meta_next[i];
+#ifdef DEC_PRIO_GATHER  // A/B builds only: w + 4 leads the next gather
+    prio_lead(wave_s & 4);
+#else
+    __builtin_amdgcn_s_setprio(0);  // the next tile's gather: equal
+#endif
   }
 #ifdef DEC_STAMP
   if ((threadIdx.x & 63) == 0)
