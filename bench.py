@@ -7,8 +7,12 @@ One step = for a batch of independent payloads already resident in HBM:
   ECCR_AMD_reconstruct_batch (random `threshold`-of-n shards -> payload)
 value = total payload bytes of all ranks / max-over-ranks step time, GiB/s.
 
-Multi-GPU: one process per GPU (torchrun), payloads sharded by rank with no
-data-path collective (weak scaling); RCCL only for the barrier / max-timing.
+Multi-GPU: one process per GPU, payloads sharded by rank with no data-path
+collective (weak scaling); RCCL only for the barrier / max-timing (and the
+separately timed scatter / gather of a GPU0-resident batch).  Under torchrun
+(WORLD_SIZE set) this process is one rank and WORLD_SIZE must equal --gpus;
+run directly with --gpus N > 1 it starts N fresh rank processes itself (before
+any GPU call), relays rank 0's JSON line and exits with the worst rank status.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with a
 `roofline` object for the dominant kernel (HIP events on the launch stream)
@@ -39,7 +43,7 @@ HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
 # exit status: 0 ok; 1 a round trip / scatter-gather check failed; 3 the RCCL
 # scatter / gather hung (watchdog); 4 it raised.  The JSON line is printed first
 # in every case, so the measurement is kept and marked.
-EXIT_CHECK, EXIT_SG_TIMEOUT, EXIT_SG_ERROR = 1, 3, 4
+EXIT_CHECK, EXIT_USAGE, EXIT_SG_TIMEOUT, EXIT_SG_ERROR = 1, 2, 3, 4
 
 
 def pmc_traffic(kernel, nv, plen, cnt, batch):
@@ -85,7 +89,8 @@ def sq_issue(kernel, nv):
             k = next(ks[n] for n in names if n in ks)  # (kernel names by round)
             return {"simd_issue_frac": round(k["frac_active_inst_any"] * waves, 3),
                     "valu_frac": round(k["frac_active_valu"] * waves, 3),
-                    "source": os.path.relpath(path, ROOT)}
+                    "measured_in_this_run": False,
+                    "source": os.path.relpath(path, ROOT) + " (stored SQ counter profile)"}
         except (OSError, KeyError, ValueError, StopIteration):
             continue
     return None
@@ -102,31 +107,41 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(nv, plen, cnt, seconds):
+def cpu_baseline(nv, plen, cnt, seconds, threads_all=None):
     """The reference ec-cpp (oracle/_ref, -O3) on this host's cores, on a
-    bounded sample of the same workload: 1 thread, then all usable cores with
-    one payload per thread.  `value` is the all-core rate; the
-    C restatement (1 thread) stands in if the reference build is absent."""
+    bounded sample of the same workload: 1 thread, then `threads` threads with
+    one payload per thread.  `threads` is the GPU box's CPU
+    share per GPU (16: the pool's rule for worker pools on a one-GPU lease),
+    or `threads_all` (--cpu-threads) when the whole host may be used; the
+    usable-CPU count and the 16-thread rate scaled to it are reported beside
+    (labelled as an extrapolation, not a measurement).  The C restatement
+    (1 thread) stands in if the reference build is absent."""
     import oracle as orc
     kind = "reference" if orc.RefEC.available() else "port"
     impl = orc.RefEC() if kind == "reference" else orc.Oracle()
     p = synth.payload(424242, plen).tobytes()
     present = synth.present_mask(10**6, nv, cnt)
     usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(usable, 16))  # the GPU box's CPU share is 16 per GPU
+    threads = max(1, threads_all or min(usable, 16))
     res = {"unit": "GiB/s", "kind": kind, "cpu_model": cpu_model(), "host_cpus_usable": usable}
     if kind == "reference":
         d1, w1, e1, r1 = impl.time_mt(nv, p, present, 1, seconds)
         dn, wn, en, rn = impl.time_mt(nv, p, present, threads, seconds)
+        rate = dn * plen / wn / 2**30
         res.update({
-            "value": round(dn * plen / wn / 2**30, 6), "cores": threads,
+            "value": round(rate, 6), "cores": threads,
             "single_thread_GiBps": round(d1 * plen / w1 / 2**30, 6),
             "single_thread_encode_GiBps": round(d1 * plen / e1 / 2**30, 6),
             "single_thread_reconstruct_GiBps": round(d1 * plen / r1 / 2**30, 6),
-            "all_core_GiBps": round(dn * plen / wn / 2**30, 6),
+            f"threads{threads}_GiBps": round(rate, 6),
+            "all_usable_cpus_GiBps_extrapolated": (None if threads >= usable else
+                                                   round(rate * usable / threads, 6)),
             "sample": f"ec-cpp -O3 (oracle/_ref): {plen} B payload encode + reconstruct from {cnt} of "
                       f"{nv} shards, repeated for ~{seconds:.0f} s on 1 thread ({d1} payloads) and on "
-                      f"{threads} threads, one payload per thread ({dn} payloads)"})
+                      f"{threads} threads, one payload per thread ({dn} payloads)"
+                      + ("" if threads >= usable else
+                         f"; {threads} = the box's CPU share per GPU of {usable} usable CPUs "
+                         "(--cpu-threads to use more)")})
         return res
     t_enc = t_dec = 0.0
     reps = 0
@@ -289,7 +304,7 @@ def size_sweep(args, nv, cnt_key, dev, stream, dist, world, rank, backend, headl
                    "roundtrip_ok": ok}
             del d_pay, d_pres, d_sh, d_el, d_out
             torch.cuda.empty_cache()
-        if rank == 0 and not args.no_cpu_baseline:
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
             row["cpu_ec_cpp"] = cpu_size_rate(nv, plen, cnt, args.sweep_cpu_seconds, threads)
         rows.append(row)
     return rows
@@ -370,6 +385,58 @@ def _scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out, step_s):
             "ok": bool(flag.item())}
 
 
+def launch_ranks(n, backend, grace_s=60.0):
+    """`python bench.py --gpus N` without a launcher: start N rank processes of
+    this script (fresh interpreters, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
+    in their environment, one per GPU: LOCAL_RANK = RANK), before this process
+    makes any GPU call (it never makes one).  Their output is inherited, so
+    rank 0's JSON line is the line printed.  Returns the worst exit status: the
+    largest non-zero one, a signal as 128 + signo; once a rank has failed the
+    others get `grace_s` to finish before they are terminated (a rank blocked
+    in a collective with a dead peer would otherwise hang)."""
+    import signal
+    import socket
+    import subprocess
+    if backend == "nccl":
+        have = torch.cuda.device_count()  # (counting does not initialise the GPU)
+        if have < n:
+            print(json.dumps({"error": f"--gpus {n} needs {n} visible GPUs, {have} found"}),
+                  file=sys.stderr, flush=True)
+            return EXIT_USAGE
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    status = {}
+    failed_at = None
+    while len(status) < n:
+        for r, p in enumerate(procs):
+            if r not in status and p.poll() is not None:
+                status[r] = p.returncode
+                if p.returncode != 0 and failed_at is None:
+                    failed_at = time.monotonic()
+        if failed_at is not None and time.monotonic() - failed_at > grace_s:
+            for r, p in enumerate(procs):
+                if r not in status:
+                    p.send_signal(signal.SIGTERM)
+            for r, p in enumerate(procs):
+                if r not in status:
+                    try:
+                        status[r] = p.wait(15)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        status[r] = p.wait()
+        time.sleep(0.05)
+    codes = [c if c >= 0 else 128 - c for c in status.values()]
+    return max(codes)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -382,6 +449,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="CPU baseline sample per leg (1 thread, all cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the multi-thread CPU baseline leg (default: min(usable, 16), "
+                         "the GPU box's CPU share per GPU)")
     ap.add_argument("--no-scatter", action="store_true",
                     help="skip the RCCL scatter / gather phase (N > 1)")
     ap.add_argument("--scatter-timeout", type=float, default=180.0)
@@ -399,12 +469,20 @@ def main():
     args.sweep_sizes = (() if args.sweep == "none" else BENCH_SIZES if args.sweep == "bench"
                         else tuple(int(x) for x in args.sweep.split(",")))
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # ECCR_BENCH_BACKEND=gloo (rehearsal only): ranks may share a GPU, the
     # barrier / max-timing run on CPU tensors.  Default: one rank per GPU, RCCL.
     backend = os.environ.get("ECCR_BENCH_BACKEND", "nccl")
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, backend))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(json.dumps({"error": f"--gpus {args.gpus} but WORLD_SIZE={world}: the launcher's "
+                                   "rank count must equal --gpus"}), file=sys.stderr, flush=True)
+        sys.exit(EXIT_USAGE)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     if backend != "nccl":
         local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
@@ -516,6 +594,7 @@ def main():
         "metric": METRIC, "value": round(value, 3), "unit": "GiB/s",
         # ranks share GPUs only in the gloo rehearsal mode (ECCR_BENCH_BACKEND)
         "n_gpus": world if backend == "nccl" else min(world, max(torch.cuda.device_count(), 1)),
+        "ranks": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u16",
@@ -531,14 +610,16 @@ def main():
                      "bytes_per_launch": b_dom, "avg_launch_ms": round(t_dom, 4),
                      "issue": sq_issue(dom, nv),
                      "measured": dict(bw, frac_of_copy=round(achieved / (bw["copy_GBps"] * 1e9), 4))},
-        # secondary ceiling: the reference algorithm's GF(2^16)
-        # multiplies per second, against the register-only multiply stream
+        # secondary figure: the REFERENCE algorithm's GF(2^16)
+        # multiplies (additive_fft.hpp:99-141) per second of our kernel time.
+        # Not a ceiling: the kernels run fewer multiplies than the reference
+        # (restricted FFT, zero skews) and most in cheaper subfield / F9 forms,
+        # so no single multiply rate bounds it; the bound is
+        # SIMD instruction issue, reported under roofline.issue
         "gf_mul": {"encode_per_s": round(B * pieces * mul_enc / (t_enc * 1e-3), -9),
                    "reconstruct_per_s": round(B * cols * mul_rec / (t_rec * 1e-3), -9),
                    "per_piece_encode": mul_enc, "per_column_reconstruct": round(mul_rec, 1),
-                   "ceiling_per_s": 6.0e12,
-                   "ceiling_source": "scripts/micro/mulrate.hip: general v_perm multiply-accumulate "
-                                     "butterflies, tables in registers, 4 waves/SIMD (DESIGN.md §6)"},
+                   "counts": "reference algorithm (ec-cpp), not the multiplies executed"},
         "kernels_ms": {"encode": round(t_enc, 4), "error_locator": round(t_loc, 4),
                        "reconstruct": round(t_rec, 4)},
         "encode_GiBps": round(world * B * plen / (t_enc * 1e-3) / 2**30, 3),
@@ -558,8 +639,9 @@ def main():
         ok = ok and all(r["roundtrip_ok"] for r in line["sizes"])
     if backend != "nccl":
         line["rehearsal"] = f"{world} ranks on {line['n_gpus']} GPU(s), gloo"
-    if rank == 0 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(nv, plen, cnt, args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # (contract: rank 0 at N = 1)
+        line["cpu_baseline"] = cpu_baseline(nv, plen, cnt, args.cpu_seconds,
+                                           args.cpu_threads or None)
     sg_failed = False
     sg_bad = False
     if dist and backend == "nccl" and not args.no_scatter:

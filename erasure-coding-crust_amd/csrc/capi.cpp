@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <optional>
 #include <string>
 #include <vector>
 
@@ -398,15 +399,19 @@ namespace {
 // records and waits on nothing (capturable into a hipGraph), and calls on
 // different streams never wait on each other.  `ok` false = too small /
 // misaligned workspace or a failed allocation: nothing may be launched.
+// Without a workspace the stream's scratch lease is held for the object's
+// lifetime, i.e. until the call has enqueued all its kernels (ec_runtime.hpp).
 struct BatchScratch {
   void *p = nullptr;
   bool ok = false;
+  std::optional<StreamScratch> lease;
   BatchScratch(DeviceState *d, size_t need, hipStream_t s, const Workspace *ws) {
     if (need == 0) {
       ok = true;
     } else if (!ws) {
-      p = stream_scratch(d, s, need);
-      ok = p != nullptr;
+      lease.emplace(d, s, need);
+      p = lease->ptr();
+      ok = lease->ok();
     } else if (!ws->ptr || ws->bytes < need || reinterpret_cast<uintptr_t>(ws->ptr) % 256 != 0) {
       set_error("erasure_coding_crust(amd): workspace of " + std::to_string(ws->bytes) +
                 " bytes (256-B aligned required) is below the " + std::to_string(need) +
@@ -628,6 +633,11 @@ NPRSResult ECCR_AMD_systematic_batch(unsigned long nv, const uint8_t *d_shards, 
 }
 
 void ECCR_AMD_set_scratch_limit(unsigned long bytes) { set_scratch_limit(bytes); }
+
+int ECCR_AMD_release_stream_scratch(void *stream) {
+  DeviceState *d = device_state();
+  return d && release_stream_scratch(d, static_cast<hipStream_t>(stream)) ? 1 : 0;
+}
 
 const char *ECCR_AMD_last_error(void) { return last_error(); }
 

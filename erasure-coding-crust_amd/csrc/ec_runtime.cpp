@@ -32,13 +32,23 @@ struct DeviceState {
   std::mutex loc_mu;
   std::list<std::shared_ptr<Locator>> loc;  // most recent first
   unsigned long loc_hits = 0, loc_misses = 0;
-  struct StreamBuf {
-    hipStream_t s;
-    void *p;
-    size_t cap;
-  };
   std::mutex ss_mu;
-  std::list<StreamBuf> ss;  // per-stream scratch, most recently used first
+  std::list<std::shared_ptr<StreamScratchEntry>> ss;  // per-stream scratch, most recent first
+};
+
+// One stream's scratch buffer.  `mu` is held by a StreamScratch lease while
+// its caller enqueues; the buffer is freed by the last owner (the device list
+// or a lease), after the device has drained (see ec_runtime.hpp).
+struct StreamScratchEntry {
+  hipStream_t s = nullptr;
+  void *p = nullptr;
+  size_t cap = 0;
+  std::mutex mu;
+  ~StreamScratchEntry() {
+    if (!p) return;
+    (void)hipDeviceSynchronize();
+    (void)hipFree(p);
+  }
 };
 
 namespace {
@@ -306,41 +316,74 @@ std::shared_ptr<const Locator> cached_locator(DeviceState *d, const CodeParams &
   return L;
 }
 
-void *stream_scratch(DeviceState *d, hipStream_t s, size_t bytes) {
-  if (bytes == 0) return nullptr;
+StreamScratch::StreamScratch(DeviceState *d, hipStream_t s, size_t bytes) : want_(bytes) {
+  if (!d || bytes == 0) return;
   const size_t limit = g_scratch_limit;
   if (limit && bytes > limit) {  // as if hipMalloc had failed
     set_error("erasure_coding_crust(amd): scratch of " + std::to_string(bytes) +
               " bytes exceeds the limit set by ECCR_AMD_set_scratch_limit");
-    return nullptr;
+    return;
   }
-  std::lock_guard<std::mutex> lk(d->ss_mu);
-  auto it = d->ss.begin();
-  while (it != d->ss.end() && it->s != s) ++it;
-  if (it != d->ss.end()) {
-    d->ss.splice(d->ss.begin(), d->ss, it);  // most recent first
-    DeviceState::StreamBuf &b = d->ss.front();
-    if (b.cap >= bytes) return b.p;
-    // grow: this stream's earlier work may still read the smaller buffer
-    if (!hip_ok(hipStreamSynchronize(s), "scratch grow sync")) return nullptr;
-    (void)hipFree(b.p);
-    b.p = nullptr;
-    b.cap = 0;
-    if (!hip_ok(hipMalloc(&b.p, bytes), "hipMalloc(stream scratch)")) return nullptr;
-    b.cap = bytes;
-    return b.p;
+  std::shared_ptr<StreamScratchEntry> evicted;  // dropped after ss_mu is released
+  {
+    std::lock_guard<std::mutex> lk(d->ss_mu);
+    auto it = d->ss.begin();
+    while (it != d->ss.end() && (*it)->s != s) ++it;
+    if (it != d->ss.end()) {
+      d->ss.splice(d->ss.begin(), d->ss, it);  // most recent first
+    } else {
+      if (d->ss.size() >= kStreamScratch) {
+        evicted = std::move(d->ss.back());
+        d->ss.pop_back();
+      }
+      auto e = std::make_shared<StreamScratchEntry>();
+      e->s = s;
+      d->ss.push_front(std::move(e));
+    }
+    e_ = d->ss.front();
   }
-  if (d->ss.size() >= kStreamScratch) {
-    // the oldest entry's stream may be gone (its handle dangling): wait for
-    // the whole device instead of that stream, then release it (rare)
-    if (!hip_ok(hipDeviceSynchronize(), "scratch evict sync")) return nullptr;
-    (void)hipFree(d->ss.back().p);
-    d->ss.pop_back();
+  evicted.reset();  // the last owner frees it (after a device synchronisation)
+  e_->mu.lock();
+  locked_ = true;
+  if (e_->cap < bytes) {
+    // every earlier holder on this stream has finished enqueueing (they held
+    // mu), so once the stream drains nothing reads the smaller buffer
+    if (e_->p) {
+      if (!hip_ok(hipStreamSynchronize(s), "scratch grow sync")) return;
+      (void)hipFree(e_->p);
+    }
+    e_->p = nullptr;
+    e_->cap = 0;
+    if (!hip_ok(hipMalloc(&e_->p, bytes), "hipMalloc(stream scratch)")) return;
+    e_->cap = bytes;
   }
-  void *p = nullptr;
-  if (!hip_ok(hipMalloc(&p, bytes), "hipMalloc(stream scratch)")) return nullptr;
-  d->ss.push_front({s, p, bytes});
-  return p;
+  p_ = e_->p;
+}
+
+StreamScratch::~StreamScratch() {
+  if (locked_) e_->mu.unlock();
+}
+
+bool release_stream_scratch(DeviceState *d, hipStream_t s) {
+  std::shared_ptr<StreamScratchEntry> e;
+  {
+    std::lock_guard<std::mutex> lk(d->ss_mu);
+    for (auto it = d->ss.begin(); it != d->ss.end(); ++it)
+      if ((*it)->s == s) {
+        e = std::move(*it);
+        d->ss.erase(it);
+        break;
+      }
+  }
+  if (!e) return false;
+  std::lock_guard<std::mutex> lk(e->mu);  // no caller is enqueueing on it
+  if (e.use_count() == 1 && e->p) {       // nobody else can reach it any more
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(e->p);
+    e->p = nullptr;
+    e->cap = 0;
+  }
+  return true;
 }
 
 void locator_cache_stats(DeviceState *d, unsigned long *hits, unsigned long *misses) {
@@ -394,18 +437,29 @@ HostCtx::~HostCtx() {
 
 bool finish_call(HostCtx *c, const char *what) {
   const auto sync = [&]() { return hip_ok(hipStreamSynchronize(c->stream), what); };
-  if (!c->h_flag &&
-      hipHostMalloc(reinterpret_cast<void **>(&c->h_flag), 64, hipHostMallocDefault) != hipSuccess) {
-    c->h_flag = nullptr;
-    return sync();
+  if (!c->h_flag) {
+    if (hipHostMalloc(reinterpret_cast<void **>(&c->h_flag), 64, hipHostMallocDefault) != hipSuccess) {
+      c->h_flag = nullptr;
+      return sync();
+    }
+    // a recycled pinned word may hold any stale value: start from a known one
+    __atomic_store_n(c->h_flag, 0u, __ATOMIC_RELEASE);
+    c->seq = 0;
   }
-  const uint32_t v = ++c->seq;
+  uint32_t v = ++c->seq;
+  if (v == 0) v = c->seq = 1;  // (wrap) 0 is the initial value
   if (launch_signal_host(c->h_flag, v, c->stream) != hipSuccess) return sync();
+  // now and then ask the stream for an asynchronous error the spin cannot see
+  const bool probe = (v & (kFinishProbeEvery - 1)) == 0;
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   for (;;) {
     for (int i = 0; i < 64; ++i)
-      if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == v) return true;
+      if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == v) {
+        if (!probe) return true;
+        const hipError_t e = hipStreamQuery(c->stream);
+        return e == hipSuccess || e == hipErrorNotReady || hip_ok(e, what);
+      }
     if (std::chrono::duration<double, std::micro>(clk::now() - t0).count() > kFinishSpinUs)
       return sync();  // long calls block instead of spinning; errors surface here
   }

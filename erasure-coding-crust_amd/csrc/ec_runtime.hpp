@@ -21,9 +21,9 @@ struct DeviceState;
 DeviceState *device_state();
 DevTables device_tables(DeviceState *d);
 const uint16_t *device_fold(DeviceState *d, uint32_t n);  // folded LOG_WALSH for n
-// Per-device scratch for the launches that need one (the k = 1024 encode's
-// coefficients between its four launches, generic kernels beyond LDS).  A
-// lease is held while a launch is enqueued: it orders the caller's stream
+// Per-device scratch of the per-call C ABI (gather orders, the k = 1024
+// encode's coefficient slots, generic kernels beyond LDS).  A lease is held
+// while a call's launches are enqueued: it orders the caller's stream
 // after the previous lease's work (an event), so launches from different
 // streams or host threads never overlap on the buffer.
 // Upper bound on one scratch allocation (0 = none): a larger request fails
@@ -49,15 +49,41 @@ class ScratchLease {
 };
 
 // Scratch private to one (device, stream), for the batch calls made without a
-// caller workspace: grown on the first call of a larger shape on that stream
-// (which synchronises the stream before the smaller buffer is freed);
-// afterwards a call allocates, records and waits on nothing, so it can be
-// captured into a hipGraph, and calls on different streams never wait on each
-// other.  At most kStreamScratch streams per device keep a buffer (the least
-// recently used beyond that is released after a device synchronisation).
-// nullptr (error set) if the allocation failed or exceeds the scratch limit.
+// caller workspace.  A StreamScratch is a lease: it holds the entry's mutex
+// from the moment the buffer is handed out until the caller has enqueued every
+// kernel that uses it (the object's lifetime), so two host threads issuing on
+// the same stream (e.g. the shared default stream) run their kernel sequences
+// one after the other on it, never interleaved on one buffer.  The buffer grows
+// on the first call of a larger shape on that stream, after synchronising the
+// stream (every earlier holder has finished enqueueing by then).  Otherwise a
+// call allocates, records and waits on nothing, so it can be captured into a
+// hipGraph, and calls on different streams never wait on each other.  At most
+// kStreamScratch streams per device keep a buffer; beyond that the least
+// recently used entry is dropped, and its buffer is freed by its last holder
+// after a hipDeviceSynchronize (the stream handle may be dangling, so the
+// whole device is waited for: rare, but it does wait on every stream).
+// ECCR_AMD_release_stream_scratch releases one stream's buffer explicitly.
+// ok() false (error set) if the allocation failed or exceeds the scratch limit.
 constexpr size_t kStreamScratch = 64;
-void *stream_scratch(DeviceState *d, hipStream_t s, size_t bytes);
+struct StreamScratchEntry;
+class StreamScratch {
+ public:
+  StreamScratch(DeviceState *d, hipStream_t s, size_t bytes);
+  ~StreamScratch();
+  StreamScratch(const StreamScratch &) = delete;
+  StreamScratch &operator=(const StreamScratch &) = delete;
+  void *ptr() const { return p_; }
+  bool ok() const { return want_ == 0 || p_ != nullptr; }
+
+ private:
+  std::shared_ptr<StreamScratchEntry> e_;  // declared first: released after the lock
+  bool locked_ = false;
+  size_t want_ = 0;
+  void *p_ = nullptr;
+};
+// Frees the scratch kept for stream s on the current device (after
+// synchronising s).  False if none was kept.
+bool release_stream_scratch(DeviceState *d, hipStream_t s);
 
 // Per-pattern erasure-locator cache of the per-call C ABI (SURVEY.md §8f
 // row 3): the locator of a pattern (n_validators + present bitmap) is computed
@@ -107,7 +133,10 @@ HostCtx *host_ctx();  // nullptr if no device
 // sequence number to the context's pinned word and the host spins on it for up
 // to kFinishSpinUs, then falls back to hipStreamSynchronize (which also
 // reports an asynchronous error).  False (error set) on a HIP error.
+// Every kFinishProbeEvery-th spin-completed call also queries the stream, so
+// an asynchronous kernel error is reported within that many calls.
 constexpr double kFinishSpinUs = 200.0;
+constexpr uint32_t kFinishProbeEvery = 16;
 bool finish_call(HostCtx *c, const char *what);
 bool ensure_host(uint8_t **p, size_t *cap, size_t need);
 bool ensure_dev(void **p, size_t *cap, size_t need);

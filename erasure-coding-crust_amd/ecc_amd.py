@@ -135,6 +135,7 @@ def lib():
             "ECCR_AMD_reconstruct_host_batch": (NPRSResult, [ul, vp, ul, ul, vp, ul, ul, vp, ul,
                                                              ul]),
             "ECCR_AMD_set_scratch_limit": (None, [ul]),
+            "ECCR_AMD_release_stream_scratch": (C.c_int, [vp]),
             "ECCR_AMD_last_error": (C.c_char_p, []),
         }
         for name, (res, args) in sig.items():
@@ -187,6 +188,11 @@ def device_count() -> int:
 
 def set_scratch_limit(nbytes: int) -> None:
     lib().ECCR_AMD_set_scratch_limit(nbytes)
+
+
+def release_stream_scratch(stream=None) -> bool:
+    """Free the batch calls' scratch kept for `stream` (default: torch's current stream)."""
+    return bool(lib().ECCR_AMD_release_stream_scratch(_stream(stream)))
 
 
 def last_error() -> str:

@@ -12,7 +12,13 @@
  * a larger shape on a stream allocates it (hipMalloc, after synchronising that
  * stream if a smaller one is replaced); afterwards the plain calls allocate,
  * record and wait on nothing, and calls on different streams never wait on
- * each other.  The *_ws variants take caller-owned scratch instead (size from
+ * each other.  Host threads may issue plain calls on the same stream
+ * concurrently: each call holds that stream's scratch until it has enqueued
+ * all its kernels, so the calls run one after the other on the stream.  A
+ * stream keeps its largest scratch until ECCR_AMD_release_stream_scratch or
+ * until more than 64 streams of the device have one: then the least recently
+ * used is released after a device-wide synchronisation (which waits for work
+ * on every stream of the device).  The *_ws variants take caller-owned scratch instead (size from
  * the matching *_workspace_bytes query) and never allocate.  Either form can
  * be captured into a hipGraph and replayed once the shape has run once on the
  * stream outside capture (the first call per (device, kernel) also sets a
@@ -184,6 +190,11 @@ struct NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long n_validators,
  * (chunk-sized) scratch and are not capped.  For memory-constrained
  * deployments and the failure-path tests. */
 void ECCR_AMD_set_scratch_limit(unsigned long bytes);
+
+/* Frees the device scratch the plain batch calls keep for `stream` on the
+ * current device (after synchronising `stream`); call it before destroying a
+ * stream that issued batch calls.  Returns 1 if a buffer was kept, else 0. */
+int ECCR_AMD_release_stream_scratch(void *stream);
 
 /* Last error message of the calling thread ("" if none). */
 const char *ECCR_AMD_last_error(void);

@@ -355,6 +355,103 @@ def test_capi_concurrent_threads(oracle):
     assert not errors, errors
 
 
+def test_batch_concurrent_default_stream(oracle):
+    """host threads issuing the plain device-batch calls at once on
+    the SAME stream (torch's default stream, handle 0) with mixed shapes, so
+    the stream's scratch is shared, grown and handed to several callers: every
+    call holds it until its kernels are enqueued, so each payload's gather
+    order and coefficient slots are its own.  Every shard and output byte vs
+    the oracle."""
+    import threading
+    shapes = [(1024, 100_001, 3), (4096, 60_001, 2), (1024, 5000, 5), (600, 70_001, 3),
+              (2500, 20_001, 2), (1024, 300_001, 2)]
+    got, errors = {}, []
+
+    def worker(tid):
+        try:
+            for rep in range(3):
+                nv, plen, batch = shapes[(tid + rep) % len(shapes)]
+                got[(tid, rep)] = (nv, plen, batch,
+                                   _batch_case(nv, plen, batch, seed0=1000 * tid + 10 * rep, pad=64))
+        except Exception as e:  # surfaced below
+            errors.append((tid, repr(e)))
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(6)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(180)
+    assert not any(t.is_alive() for t in threads)
+    assert not errors, errors
+    assert len(got) == 18
+    for (tid, rep), (nv, plen, batch, (pay, pres, sh, el, out)) in sorted(got.items()):
+        for b in range(batch):
+            ref = oracle.encode(nv, pay[b].tobytes())
+            assert b"".join(ref) == sh[b].tobytes(), (tid, rep, b)
+            keep = [ref[i] if pres[b][i] else None for i in range(nv)]
+            assert out[b].tobytes() == oracle.reconstruct(nv, keep), (tid, rep, b)
+
+
+def test_release_stream_scratch():
+    """ECCR_AMD_release_stream_scratch frees a stream's batch scratch; the next
+    call on that stream allocates it again and is still correct."""
+    import torch
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        pay, pres, sh, el, out = _batch_case(1024, 100_001, 2, seed0=55, pad=64)
+    assert E.release_stream_scratch(s)
+    assert not E.release_stream_scratch(s)
+    with torch.cuda.stream(s):
+        pay2, pres2, sh2, el2, out2 = _batch_case(1024, 100_001, 2, seed0=55, pad=64)
+    torch.cuda.synchronize()
+    assert (out2 == out).all() and (out2[:, :100_001] == pay2).all()
+    E.release_stream_scratch(s)
+
+
+@pytest.mark.parametrize("nv", [1024, 4096])
+def test_batch_past_4GiB(oracle, nv):
+    """both headline workloads address shard bytes beyond
+    2^32 (config 2: 16.6 GB of shards).  B = 1100 x 1 MB with 64-B rows puts
+    4.47 GB (nv = 1024) / 4.6 GB (nv = 4096) of shards on the device; payloads
+    0 and B - 1 and the payloads on either side of (and straddling) the 2^32
+    byte offset are compared byte for byte with the oracle (encode and
+    reconstruct, reed-solomon.hpp:73-78,116-127); every payload round-trips."""
+    import torch
+    plen, batch = 1_000_000, 1100
+    n, k, thr = E.code_params(nv)
+    sl = E.shard_len(nv, plen)
+    ss = (sl + 63) // 64 * 64
+    row = nv * ss  # shard bytes per payload
+    assert batch * row > (1 << 32)
+    seeds = list(range(77_000, 77_000 + batch))
+    d_pay = torch.empty((batch, plen), dtype=torch.uint8, device="cuda")
+    for c0 in range(0, batch, 256):
+        d_pay[c0:c0 + 256] = synth.payloads_torch(seeds[c0:c0 + 256], plen)
+    pres = synth.present_masks([10**6 + s for s in seeds], nv, thr, n)
+    d_pr = torch.from_numpy(pres).cuda()
+    d_sh = _prefilled((batch, nv, ss))
+    d_el = torch.zeros((batch, n), dtype=torch.int16, device="cuda")
+    d_out = _prefilled((batch, sl * k))
+    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+    E.error_locator(nv, d_pr, batch, d_el)
+    E.reconstruct_batch(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k)
+    torch.cuda.synchronize()
+    assert torch.equal(d_out[:, :plen], d_pay)
+    assert not d_out[:, plen:].any()
+    edge = (1 << 32) // row  # the payload whose shard rows reach / straddle 2^32
+    check = sorted({0, batch - 1, edge - 1, edge, edge + 1})
+    assert any(b * row < (1 << 32) <= (b + 1) * row for b in check)
+    for b in check:
+        p = synth.payload(seeds[b], plen).tobytes()
+        assert d_pay[b].cpu().numpy().tobytes() == p
+        ref = oracle.encode(nv, p)
+        assert b"".join(ref) == d_sh[b, :, :sl].cpu().numpy().tobytes(), b
+        keep = [ref[i] if pres[b][i] else None for i in range(nv)]
+        assert d_out[b].cpu().numpy().tobytes() == oracle.reconstruct(nv, keep), b
+    del d_pay, d_sh, d_out
+    torch.cuda.empty_cache()
+
+
 # ------------------------------------------- erasure patterns per reconstruct kernel
 def _pattern_rows(nv, n, k, thr, rng):
     """One present mask per pattern the reference's gap / erased-index handling

@@ -45,6 +45,26 @@ def test_bench_two_ranks_share_gpu():
     assert line["value"] > 0 and line["steps"] == 2
 
 
+def test_bench_gpus_flag_launches_ranks():
+    """The driver's command form without a launcher: `python3 bench.py --gpus 2`
+    must start 2 rank processes itself, not measure one
+    GPU and call it two.  gloo rehearsal (both ranks on the box's one GPU)."""
+    env = dict(os.environ, ECCR_BENCH_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--batch", "48", "--payload", "100000", "--no-cpu-baseline", "--sweep", "none"]
+    r = subprocess.run(["timeout", "-k", "10", "300"] + cmd, cwd=ROOT, env=env,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0's line only
+    line = lines[0]
+    assert line["config"]["parallelism"] == "dp2" and line["ranks"] == 2, line
+    assert line["roundtrip_ok"] and "gloo" in line["rehearsal"], line
+    assert line["value"] > 0 and line["steps"] == 2
+
+
 def test_bench_stream_two_ranks_share_gpu():
     r, line = _torchrun([os.path.join("scripts", "bench_stream.py"), "--per-size", "2", "--reps", "1"])
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
