@@ -261,11 +261,7 @@ __device__ __forceinline__ uint32_t tower_lo(uint32_t l, uint32_t h, const Tower
 // LDS address `a` (plane 0).
 template <int PLANE>
 __device__ __forceinline__ void lds_subtab_abs(uint32_t a, SubTab &T) {
-#ifdef DIAG_SUB_NOCONFLICT  // diagnostic builds only (wrong results): conflict-free plane-1 reads
-  T.t[4] = *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t(PLANE + 4 * __builtin_amdgcn_mbcnt_lo(~0u, 0)));
-#else
   T.t[4] = *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t(a + PLANE));
-#endif
   typedef uint32_t v4u __attribute__((ext_vector_type(4)));
   const v4u v = *(const __attribute__((address_space(3))) v4u *)(uintptr_t(a));
   T.t[0] = v.x;

@@ -35,6 +35,25 @@ constexpr bool f9_slot(int kind, uint32_t i) {
   return i % 4 == 1 || (kind == 1 && i % 2 == 0 && i >= 256 && i < 512);
 }
 
+// Element-indexed compact image (the n = 1024 encode).  The
+// skew of a stage-m butterfly at position pos of an FFT / IFFT at index `off`
+// (additive_fft.hpp:99-141) is the element 2 x, x = (pos + off) >> (m + 1)
+// (skews[i] = log(((i + 1) >> ctz(i + 1)) - 1); checked against the oracle),
+// so a table set can be indexed by x instead of by skew slot.  For the
+// k = 256 / n = 1024 encode x < 512, and the element's tower coordinates put
+// it in one of three kinds: x < 128 subfield (MulTabSub), 128 <= x < 256 F9
+// (MulTabF9), 256 <= x < 512 general (Field::tower_tab).  Plane q of entry x
+// sits at base(kind, q) | cimg_lin(x ^ kind_bit), cimg_lin GF(2)-linear (the
+// LdsTabs swizzle applied to x), so every table address is a per-lane base XOR
+// a wave-uniform value; 32 KB instead of the 80 KB skew-slot image.
+constexpr uint32_t kCImgGen = 0, kCImgGenPlane = 4096;      // 5 planes x 256 entries
+constexpr uint32_t kCImgF9 = 20480, kCImgF9Plane = 2048;    // 4 planes x 128 entries
+constexpr uint32_t kCImgSub0 = 28672, kCImgSub1 = 30720;    // plane 0 / dword 0 of plane 1, 128 entries
+constexpr uint32_t kCImgBytes = 32768;
+__host__ __device__ constexpr uint32_t cimg_lin(uint32_t x) {
+  return ((x >> 4) << 8) | (((x ^ (x >> 4) ^ (x >> 8)) & 15) << 4);
+}
+
 struct DevTables {
   const uint16_t *skews = nullptr;     // 65535
   const MulTab *mtab = nullptr;        // 65536
@@ -43,6 +62,7 @@ struct DevTables {
   const MulTab *mtab_tout = nullptr;   // 65536, tower in, symbols out
   const uint8_t *timg_t = nullptr;     // kTabImages x kTabImageBytes, tower images
   const uint8_t *timg_f9 = nullptr;    // kF9Images x kTabImageBytes, F9 variants of tower image 0
+  const uint8_t *cimg = nullptr;       // kCImgBytes, the element-indexed compact image
 };
 
 // Per (device, kernel), once and thread-safe: raise `fn`'s dynamic-LDS limit
@@ -105,6 +125,11 @@ bool k256_packed_ok(size_t plen, size_t batch, uintptr_t sh, size_t sstride);
 hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                               size_t sstride, hipStream_t s);
+// the n = 1024, unpacked case of launch_encode_k256: two 8-wave workgroups per
+// CU on the compact image (enc_k256w.hip)
+hipError_t launch_encode_k256w(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
+                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
+                               size_t sstride, hipStream_t s);
 
 // specialised kernels (enc_k1024.hip): k = 1024, n = 4096, needs a coefficient
 // scratch of k1024_scratch_bytes

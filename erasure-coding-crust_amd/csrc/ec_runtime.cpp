@@ -22,6 +22,7 @@ struct DeviceState {
   MulTab *mtab_t = nullptr;  // mtab_tin, then mtab_tout
   uint8_t *timg_t = nullptr;
   uint8_t *timg_f9 = nullptr;
+  uint8_t *cimg = nullptr;
   std::mutex mu;
   std::map<uint32_t, uint16_t *> fold;
   std::mutex scratch_mu;  // held by a ScratchLease
@@ -128,6 +129,29 @@ DeviceState *device_state() {
         std::memcpy(&img_f9[slot + plane * 16384], &t9.w[4 * plane], 16);
     }
   }
+  // the element-indexed compact image (ec_kernels.hpp): entry x = element 2 x
+  std::vector<uint8_t> cimg(kCImgBytes, 0);
+  for (uint32_t x = 0; x < 512; ++x) {
+    const uint32_t e = 2 * x, c = e == 0 ? kZeroTab : f.log[e];
+    if (x < 128) {
+      const MulTabSub u = f.sub_tab(c);
+      std::memcpy(&cimg[kCImgSub0 | cimg_lin(x)], &u.w[0], 16);
+      std::memcpy(&cimg[kCImgSub1 | cimg_lin(x)], &u.w[4], 4);
+    } else if (x < 256) {
+      MulTabF9 t9;
+      if (!f.f9_tab(c, &t9)) return nullptr;  // (tower(e) >> 8 == 1 for 256 <= e < 512)
+      for (uint32_t q = 0; q < 4; ++q)
+        std::memcpy(&cimg[(kCImgF9 + q * kCImgF9Plane) | cimg_lin(x ^ 128)], &t9.w[4 * q], 16);
+    } else {
+      const MulTab g = f.tower_tab(c);
+      for (uint32_t q = 0; q < 5; ++q)
+        std::memcpy(&cimg[(kCImgGen + q * kCImgGenPlane) | cimg_lin(x ^ 256)], &g.w[4 * q], 16);
+    }
+  }
+  if (!hip_ok(hipMalloc(&st->cimg, cimg.size()), "hipMalloc(compact image)") ||
+      !hip_ok(hipMemcpy(st->cimg, cimg.data(), cimg.size(), hipMemcpyHostToDevice),
+              "upload compact image"))
+    return nullptr;
   if (!hip_ok(hipMalloc(&st->timg_f9, img_f9.size()), "hipMalloc(F9 images)") ||
       !hip_ok(hipMemcpy(st->timg_f9, img_f9.data(), img_f9.size(), hipMemcpyHostToDevice),
               "upload F9 images"))
@@ -168,6 +192,7 @@ DevTables device_tables(DeviceState *d) {
   t.mtab_tout = d->mtab_t + kFieldSize;
   t.timg_t = d->timg_t;
   t.timg_f9 = d->timg_f9;
+  t.cimg = d->cimg;
   return t;
 }
 
@@ -198,14 +223,16 @@ hipError_t prepare_kernel(const void *fn, int lds_bytes, int *cus) {
     c = cu_count.emplace(dev, n).first;
   }
   bool &done = prepared[{dev, fn}];
-  if (!done && lds_bytes > 65536) {
+  if (!done && lds_bytes >= 65536) {
     // these kernels address their multiply tables by absolute LDS address,
     // assuming their dynamic LDS starts at 0, i.e. no static LDS (lds_tab_at)
     hipFuncAttributes attr{};
     if (const hipError_t e = hipFuncGetAttributes(&attr, fn); e != hipSuccess) return e;
     if (attr.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
-    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-    if (e != hipSuccess) return e;
+    if (lds_bytes > 65536) {
+      const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+      if (e != hipSuccess) return e;
+    }
   }
   done = true;
   *cus = c->second;

@@ -23,6 +23,7 @@
 
 #include "ec_device.hpp"
 #include "ec_kernels.hpp"
+#include "enc_k256_common.hpp"
 
 namespace ecamd {
 namespace {
@@ -30,7 +31,6 @@ namespace {
 constexpr int K = 256;
 // one byte-planar group per lane (GP = 1) and 16 waves: 4 waves/SIMD (<= 128
 // VGPRs) for latency hiding; the tile is 128 pieces
-constexpr int GP = 1;
 constexpr int WAVES = 16 / GP;
 constexpr int THREADS = 64 * WAVES;
 constexpr int TILE = 8 * GP * WAVES;  // pieces per tile
@@ -40,10 +40,6 @@ constexpr int XCH_BYTES = 256 * 16 * GP;   // per-wave exchange region
 constexpr int LDS_BYTES = TAB_REGION + WAVES * XCH_BYTES;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 static_assert(TILE == 128 && 256 * 256 <= WAVES * XCH_BYTES, "staging fits the exchange regions");
-
-struct State {
-  uint32_t l[GP][8], h[GP][8];  // [group][register]: low / high byte planes
-};
 
 // GF(2)-linear part of the swizzled table address (LdsTabs::addr without the
 // plane term): tlin(a | b) = tlin(a) ^ tlin(b) for disjoint a, b.  A table index
@@ -66,11 +62,7 @@ __device__ __forceinline__ void lds_tab_at(const uint8_t *lds, uint32_t lin, Tab
 
 // subfield table (tower image): plane 0 and dword 0 of plane 1
 __device__ __forceinline__ void lds_tab_at(const uint8_t *lds, uint32_t lin, SubTab &T) {
-#ifdef DIAG_SUB_NOCONFLICT  // diagnostic builds only (wrong results): conflict-free plane-1 reads
-  T.t[4] = *reinterpret_cast<const uint32_t *>(lds + Tabs::kPlane + 4 * __builtin_amdgcn_mbcnt_lo(~0u, 0));
-#else
   T.t[4] = *reinterpret_cast<const uint32_t *>(lds + Tabs::kPlane + lin);
-#endif
   const uint4 v = *reinterpret_cast<const uint4 *>(lds + lin);
   T.t[0] = v.x;
   T.t[1] = v.y;
@@ -91,10 +83,7 @@ using TabAt = typename TabSel<(M >= SM)>::type;
 // F9 tables (F9 image kind 1) where F is set
 template <int M, int SM, bool F>
 using TabAtF = std::conditional_t<F, F9Tab, TabAt<M, SM>>;
-#ifndef ENC_F9
-#define ENC_F9 1
-#endif
-constexpr bool kF9 = ENC_F9 != 0;
+constexpr bool kF9 = true;
 
 __device__ __forceinline__ void lds_tab_at(const uint8_t *lds, uint32_t lin, F9Tab &T) {
 #pragma unroll
@@ -107,42 +96,10 @@ __device__ __forceinline__ void lds_tab_at(const uint8_t *lds, uint32_t lin, F9T
   }
 }
 
-__device__ __forceinline__ void mul_any(uint32_t xl, uint32_t xh, const Tab &T, uint32_t &yl, uint32_t &yh) {
-  mul_acc(xl, xh, T, yl, yh);
-}
-__device__ __forceinline__ void mul_any(uint32_t xl, uint32_t xh, const SubTab &T, uint32_t &yl,
-                                        uint32_t &yh) {
-  mul_acc_sub(xl, xh, T, yl, yh);
-}
-__device__ __forceinline__ void mul_any(uint32_t xl, uint32_t xh, const F9Tab &T, uint32_t &yl,
-                                        uint32_t &yh) {
-  mul_acc_f9(xl, xh, T, yl, yh);
-}
-
 // skew index of the block holding position pos_a at stage m (additive_fft.hpp:108,126)
 __device__ __forceinline__ uint32_t skew_idx(uint32_t pos_a, int m, uint32_t offset) {
   const uint32_t d = 1u << m;
   return (pos_a & ~(2 * d - 1)) + d - 1 + offset;
-}
-
-template <typename T>
-__device__ __forceinline__ void ibfly(State &s, int ra, int rb, const T &Tb) {
-#pragma unroll
-  for (int g = 0; g < GP; ++g) {
-    s.l[g][rb] ^= s.l[g][ra];
-    s.h[g][rb] ^= s.h[g][ra];
-    mul_any(s.l[g][rb], s.h[g][rb], Tb, s.l[g][ra], s.h[g][ra]);
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ void fbfly(State &s, int ra, int rb, const T &Tb) {
-#pragma unroll
-  for (int g = 0; g < GP; ++g) {
-    mul_any(s.l[g][rb], s.h[g][rb], Tb, s.l[g][ra], s.h[g][ra]);
-    s.l[g][rb] ^= s.l[g][ra];
-    s.h[g][rb] ^= s.h[g][ra];
-  }
 }
 
 // Table loads are software-pipelined: the next butterfly group's table is
@@ -233,14 +190,6 @@ __device__ __forceinline__ void fpass3(State &s, const uint8_t *tabs, uint32_t b
   }
 }
 
-__device__ __forceinline__ void bxor(State &s, int ra, int rb) {  // b ^= a (no multiply)
-#pragma unroll
-  for (int g = 0; g < GP; ++g) {
-    s.l[g][rb] ^= s.l[g][ra];
-    s.h[g][rb] ^= s.h[g][ra];
-  }
-}
-
 // layout C: register bit0 = p6, bit1 = p7, bit2 = p5 (passenger); stages 6, 7
 // have lane-uniform skews.  Only the IFFT at index 0 runs here, where the
 // block at j = d of a stage has skew skews[d - 1] = 0xFFFF (inverse_afft skips
@@ -259,17 +208,6 @@ __device__ __forceinline__ void ipassC0(State &s, const uint8_t *tabs) {
   bxor(s, 5, 7);
 }
 
-// stage-7 butterfly reading the IFFT coefficients c and writing s (stage 7
-// touches every register, so the coset needs no copy of c)
-template <typename T>
-__device__ __forceinline__ void fbfly_from(State &s, const State &c, int ra, int rb, const T &Tb) {
-  s.l[0][ra] = c.l[0][ra];
-  s.h[0][ra] = c.h[0][ra];
-  mul_any(c.l[0][rb], c.h[0][rb], Tb, s.l[0][ra], s.h[0][ra]);
-  s.l[0][rb] = c.l[0][rb] ^ s.l[0][ra];
-  s.h[0][rb] = c.h[0][rb] ^ s.h[0][ra];
-}
-
 __device__ __forceinline__ void fpassC(State &s, const State &c, const uint8_t *tabs, uint32_t off) {
   SubTab Ta, Tb;  // stages 7, 6 >= tower_sub_min(0), tower_sub_min(1)
   lds_tab_at(tabs, tlin(skew_idx(0, 7, off)), Ta);
@@ -283,70 +221,6 @@ __device__ __forceinline__ void fpassC(State &s, const State &c, const uint8_t *
   fbfly(s, 4, 5, Tb);
   fbfly(s, 2, 3, Ta);
   fbfly(s, 6, 7, Ta);
-}
-
-// position held in register r by lane q (0..31) in each layout
-__device__ __forceinline__ uint32_t posA(uint32_t q, int r) { return (q << 3) | uint32_t(r); }
-__device__ __forceinline__ uint32_t posB(uint32_t q, int r) {
-  return ((q >> 3) << 6) | (uint32_t(r) << 3) | (q & 7);
-}
-// ---- wave-private exchange -------------------------------------------------
-// 8-byte cell u = pos*2 + inst mapped by a GF(2)-linear bijection M
-// (found by search, scripts/search_swizzle.py) under which every layout's
-// reads (32-lane groups) and writes (16-lane groups) are bank-conflict free.
-// u = lane part XOR register part, so addr = M(lane part) ^ M(r part).
-constexpr uint32_t kM[9] = {0b110011100, 0b1001101, 0b111110100, 0b110001111, 0b11110011,
-                            0b101101010, 0b110000111, 0b111011000, 0b111100000};
-__host__ __device__ constexpr uint32_t mswz(uint32_t u) {
-  uint32_t a = 0;
-  for (int i = 0; i < 9; ++i) a |= uint32_t(__builtin_popcount(kM[i] & u) & 1) << i;
-  return a << 3;
-}
-// lane part / register part of u for each layout
-__device__ __forceinline__ uint32_t ulaneA(uint32_t q, uint32_t inst) { return (q << 4) | inst; }
-__device__ __forceinline__ uint32_t ulaneB(uint32_t q, uint32_t inst) {
-  return ((q >> 3) << 7) | ((q & 7) << 1) | inst;
-}
-__device__ __forceinline__ uint32_t ulaneC(uint32_t q, uint32_t inst) { return (q << 1) | inst; }
-__host__ __device__ constexpr uint32_t uregA(int r) { return uint32_t(r) << 1; }
-__host__ __device__ constexpr uint32_t uregB(int r) { return uint32_t(r) << 4; }
-__host__ __device__ constexpr uint32_t uregC(int r) {
-  return (uint32_t(r & 3) << 7) | (uint32_t(r >> 2) << 6);
-}
-
-enum Layout { LA, LB, LC };
-
-struct XBase {  // per-lane exchange base addresses
-  uint32_t a, b, c;
-};
-
-template <Layout L>
-__device__ __forceinline__ uint32_t xcell(const XBase &xb, int r) {
-  if constexpr (L == LA) return xb.a ^ mswz(uregA(r));
-  else if constexpr (L == LB) return xb.b ^ mswz(uregB(r));
-  else return xb.c ^ mswz(uregC(r));
-}
-
-template <Layout FROM, Layout TO>
-__device__ __forceinline__ void exchange(State &s, uint8_t *xch, const XBase &xb) {
-#pragma unroll
-  for (int r = 0; r < 8; ++r)
-    *reinterpret_cast<uint2 *>(xch + xcell<FROM>(xb, r)) = make_uint2(s.l[0][r], s.h[0][r]);
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const uint2 v = *reinterpret_cast<const uint2 *>(xch + xcell<TO>(xb, r));
-    s.l[0][r] = v.x;
-    s.h[0][r] = v.y;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// byte-planar group (4 pieces) -> big-endian u16 x4 (pieces 0..3 in order)
-__device__ __forceinline__ uint2 to_be(uint32_t l, uint32_t h) {
-  return make_uint2(vperm(l, h, 0x05010400u), vperm(l, h, 0x07030602u));
 }
 
 // ---- own-region staging: wave w stages its 8 pieces x 256 rows in
@@ -423,11 +297,7 @@ __device__ __forceinline__ void store_rows_fast(const uint8_t *xbase, uint8_t *S
   for (int it = 0; it < 256 / (4 * WAVES); ++it) {  // soff is GF(2)-linear in v = it * 4 WAVES | v0
     const v4u val = *(const __attribute__((address_space(3))) v4u *)(uintptr_t(sa ^ soff(uint32_t(it) * 4 * WAVES, 0)));
     // streaming (non-temporal): rows are written once, not re-read
-#ifdef ENC_PLAIN_STORES  // A/B builds only
-    *reinterpret_cast<v4u *>(dst + it * dstep) = val;
-#else
     __builtin_nontemporal_store(val, reinterpret_cast<v4u *>(dst + it * dstep));
-#endif
   }
 }
 
@@ -474,28 +344,6 @@ __device__ __forceinline__ void store_own(const uint8_t *xbase, uint8_t *SH, uin
         *reinterpret_cast<uint16_t *>(dst + 2 * e) = uint16_t(w[e >> 1] >> (16 * (e & 1)));
     }
   }
-}
-
-// 16 payload bytes at any address, zero past `avail` (bytes valid from p):
-// aligned dwords that each hold at least one wanted byte (so nothing outside
-// the payload's allocation is touched), funnel-shifted by v_alignbyte
-__device__ __forceinline__ uint4 load16_any(const uint8_t *p, uint64_t avail) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  if (avail >= 16 && (a & 15) == 0) return *reinterpret_cast<const uint4 *>(p);
-  if (avail == 0) return make_uint4(0, 0, 0, 0);
-  const uint32_t sh = uint32_t(a & 3), nb = avail < 16 ? uint32_t(avail) : 16u;
-  const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
-  uint32_t d[5];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) d[i] = uint32_t(4 * i) < sh + nb ? q[i] : 0u;
-  uint32_t w[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
-    const uint32_t have = nb > uint32_t(4 * j) ? nb - uint32_t(4 * j) : 0u;  // valid bytes of word j
-    if (have < 4) w[j] &= (1u << (8 * have)) - 1u;
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // packed waves (PK = 2): this wave's 8 staged pieces x 256 rows [s0, s0 + 256)
@@ -808,10 +656,10 @@ hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uin
   int cus = 0;
   const bool packed = k256_packed(plen, pstride, batch, reinterpret_cast<uintptr_t>(d_payloads),
                                   reinterpret_cast<uintptr_t>(d_shards), sstride);
+  if (p.n == 1024 && !packed) return launch_encode_k256w(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
   if (packed && !k256_packed_ok(plen, batch, reinterpret_cast<uintptr_t>(d_shards), sstride))
     return hipErrorInvalidValue;
-  const void *fn = p.n == 1024 ? (packed ? reinterpret_cast<const void *>(&encode_k256<1024, 2>)
-                                         : reinterpret_cast<const void *>(&encode_k256<1024, 0>))
+  const void *fn = p.n == 1024 ? reinterpret_cast<const void *>(&encode_k256<1024, 2>)
                                : (packed ? reinterpret_cast<const void *>(&encode_k256<2048, 1>)
                                          : reinterpret_cast<const void *>(&encode_k256<2048, 0>));
   if (const hipError_t e = prepare_kernel(fn, LDS_BYTES, &cus); e != hipSuccess) return e;
@@ -826,8 +674,7 @@ hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uin
                      uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride), \
                      int(p.nv), uint32_t(batch), uint32_t(npp8), t)
   if (p.n == 1024) {
-    if (packed) ECAMD_K256(1024, 2);
-    else ECAMD_K256(1024, 0);
+    ECAMD_K256(1024, 2);  // (packed: the unpacked n = 1024 case is encode_k256w)
   } else {
     if (packed) ECAMD_K256(2048, 1);
     else ECAMD_K256(2048, 0);

@@ -9,7 +9,8 @@ are in KiB summed over the TCC instances.  FETCH_SIZE reports half the bytes of
 reconstruct kernel's 64-B-per-lane row reads (/1.043).  WRITE_SIZE is exact for
 the 16-B-per-lane stores.
   encode:       fetch = raw x 2 (payload reads are 16 B per lane)
-  reconstruct:  fetch = raw / 1.043.  (Until r02 the kernel re-read the
+  reconstruct:  fetch = raw / 1.043 (reconstruct_n1024 and _n4096 alike: both
+                read 64 B of a row per lane).  (Until r02 the kernel re-read the
                 present data rows y < k in phase 5, 8 B per lane, and this
                 added them back as p5 = B x (present rows < k) x shard_len at
                 half weight.  Since r02 those rows are staged in LDS; the raw
@@ -29,6 +30,8 @@ thr = (NV - 1) // 3 + 1
 K = 1 << (thr.bit_length() - 1)
 SL = ((P + 2 * K - 1) // (2 * K)) * 2
 KERNELS = {"encode_k256": "encode", "reconstruct_n1024": "reconstruct",
+           "encode_k1024": "encode", "reconstruct_n4096": "reconstruct",
+           "encode_gen": "encode", "reconstruct_gen": "reconstruct",
            "encode_g": "encode", "reconstruct_g": "reconstruct", "error_locator_g": "error_locator"}
 
 

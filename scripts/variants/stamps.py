@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Diagnostic variants with per-phase s_memtime stamps (results unchanged; the
+product sources carry no switches: this script writes patched copies).
+
+  stamps.py enc OUT.hip   encode_k256: load / barrier wait / row stores / compute
+  stamps.py dec OUT.hip   reconstruct_n1024: gather / barrier waits / IFFT /
+                          derivative+FFT / output
+
+Each variant sums the cycles of every wave into a __device__ array and exports
+ECCR_DIAG_stamps(out, n, reset) (scripts/variants/stamp_run.py reads it).
+Build with scripts/build_var.sh NAME "" enc_k256.hip=OUT.hip (or dec_n1024.hip)."""
+import sys
+
+ROOT = __file__.rsplit("/scripts/", 1)[0]
+kind, out = sys.argv[1], sys.argv[2]
+READER = '''
+namespace ecamd {
+__device__ unsigned long long g_stamp[16];
+}
+extern "C" int ECCR_DIAG_stamps(unsigned long long *out, int n, int reset) {
+  if (n > 16) n = 16;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ecamd::g_stamp), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ecamd::g_stamp), z, sizeof(z));
+  }
+  return n;
+}
+'''
+DECL = ('namespace ecamd {\n__device__ unsigned long long g_stamp[16];\n}\n')
+STAMP = ('  uint64_t st_last_ = __builtin_amdgcn_s_memtime(), acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};\n'
+         '  const auto STAMP = [&](int i) __attribute__((always_inline)) {\n'
+         '    const uint64_t now_ = __builtin_amdgcn_s_memtime();\n'
+         '    acc_[i] += now_ - st_last_;\n'
+         '    st_last_ = now_;\n'
+         '  };\n')
+FLUSH = ('  if ((threadIdx.x & 63) == 0)\n'
+         '    for (int i = 0; i < 8; ++i) atomicAdd(&g_stamp[i], (unsigned long long)acc_[i]);\n')
+
+
+def rep(s, old, new, count=1):
+    assert s.count(old) >= count, old[:80]
+    return s.replace(old, new, count)
+
+
+if kind == "enc":
+    s = open(f"{ROOT}/erasure-coding-crust_amd/csrc/enc_k256.hip").read()
+    s = rep(s, "namespace ecamd {\nnamespace {", "namespace ecamd {\n__device__ unsigned long long g_stamp[16];\nnamespace {")
+    s = rep(s, "  Tabs::copy_image<THREADS>(tabs, img0, tid0);\n  __syncthreads();\n",
+            "  Tabs::copy_image<THREADS>(tabs, img0, tid0);\n  __syncthreads();\n" + STAMP)
+    s = rep(s, "    } else {\n      lds_barrier();\n    }\n  };",
+            "    } else {\n      STAMP(3);\n      lds_barrier();\n      STAMP(1);\n    }\n  };")
+    s = rep(s, "      __builtin_amdgcn_s_setprio(1);\n",
+            "      STAMP(3);\n      __builtin_amdgcn_s_setprio(1);\n")
+    s = rep(s, "      __builtin_amdgcn_s_setprio(0);\n    };",
+            "      __builtin_amdgcn_s_setprio(0);\n      STAMP(2);\n    };")
+    s = rep(s, "    // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)\n",
+            "    STAMP(0);\n    // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)\n")
+    # end of the tile loop body of the kernel: the two closing braces before k256_applicable
+    s = rep(s, "  }\n}\n\nbool k256_applicable", "  }\n" + FLUSH + "}\n\nbool k256_applicable")
+    names = ["load", "barrier", "stores", "compute"]
+elif kind == "dec":
+    s = open(f"{ROOT}/erasure-coding-crust_amd/csrc/dec_n1024.hip").read()
+    s = rep(s, "namespace ecamd {\nnamespace {", "namespace ecamd {\n__device__ unsigned long long g_stamp[16];\nnamespace {")
+    s = rep(s, "  Tabs::copy_image<THREADS>(tabs, kF9 ? t.timg_f9 : t.timg_t, tid0);  // F9 kind 0\n  __syncthreads();\n",
+            "  Tabs::copy_image<THREADS>(tabs, kF9 ? t.timg_f9 : t.timg_t, tid0);  // F9 kind 0\n  __syncthreads();\n" + STAMP)
+    s = rep(s, "    if ((meta[0] & 0xffffu) != 0xffffu) load_row(0);\n    lds_barrier();",
+            "    if ((meta[0] & 0xffffu) != 0xffffu) load_row(0);\n    STAMP(0);\n    lds_barrier();\n    STAMP(1);")
+    s = rep(s, "    if constexpr (!PACKED) __syncthreads();  // packed",
+            "    STAMP(0);\n    if constexpr (!PACKED) __syncthreads();\n    STAMP(1);  // packed")
+    s = rep(s, "    prio_lead(wave_s & 4);\n    // ---- phases 3 + 4a", "    prio_lead(wave_s & 4);\n    STAMP(2);\n    // ---- phases 3 + 4a")
+    s = rep(s, "    prio_lead(!(wave_s & 4));  // the output", "    STAMP(3);\n    prio_lead(!(wave_s & 4));  // the output")
+    s = rep(s, "    __builtin_amdgcn_s_setprio(0);  // the next tile's gather: equal\n  }\n",
+            "    __builtin_amdgcn_s_setprio(0);  // the next tile's gather: equal\n    STAMP(4);\n  }\n" + FLUSH)
+    names = ["gather", "barriers", "ifft", "deriv+fft", "output"]
+else:
+    sys.exit("kind: enc | dec")
+s += READER.replace('namespace ecamd {\n__device__ unsigned long long g_stamp[16];\n}\n', '')
+open(out, "w").write(s)
+print(",".join(names))
