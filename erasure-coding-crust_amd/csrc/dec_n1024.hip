@@ -20,7 +20,6 @@
 
 #include <cstdlib>
 
-#include "cimg.hpp"
 #include "ec_device.hpp"
 #include "ec_kernels.hpp"
 
@@ -670,8 +669,6 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       const uint32_t hi27 = lane << 2;
       auto L = [&](int i) -> uint32_t {
         switch (i) {
-          case 0: return tlin(skew_idx(0, 7));
-          case 1: return tlin(skew_idx(0, 6));
           case 2: return tlin(skew_idx(1u << 7, 6));
           case 3: return tlin(skew_idx(hi67 | lo, 5));
           case 4: return tlin(skew_idx(hi67 | lo, 4));
@@ -686,14 +683,18 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
           default: return tlin(sub_alias(hi27 | 2u, 0));
         }
       };
+      // stage 7 (block j = 128) and stage 6's first block (j = 64) have the
+      // skew 0xFFFF at index 0 (additive_fft.hpp:129): b ^= a only
+      const auto fx = [&](int a, int bb) {
+        ql[bb] ^= ql[a];
+        qh[bb] ^= qh[a];
+      };
       SubTab T[2];
-      tab_at(tabs, L(0), T[0]);
-      tab_at(tabs, L(1), T[1]);
-      fb(0, 2, T[0]);  // stage 7
-      fb(1, 3, T[0]);
       tab_at(tabs, L(2), T[0]);
-      fb(0, 1, T[1]);  // stage 6
       tab_at(tabs, L(3), T[1]);
+      fx(0, 2);  // stage 7
+      fx(1, 3);
+      fx(0, 1);  // stage 6
       fb(2, 3, T[0]);
       tab_at(tabs, L(4), T[0]);
       // q (p6, p7) <-> lane bits 4, 5 (p4, p5)
@@ -796,524 +797,6 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
   }
 }
 
-// ============================================================================
-// reconstruct_n1024w: the n = 1024 reconstruct as TWO 4-wave workgroups per
-// CU.  Per tile of 16 shard columns the phases are those of
-// reconstruct_n1024 above, but
-//  * the IFFT_1024 runs in layouts whose register bits hold every position bit
-//    that selects a multiply's kind (A': p0 p1 p8 p9, B': p2..p5, C: p8 p9 p6
-//    p7), so its tables come from the 32 KB element-indexed compact image
-//    (ec_kernels.hpp kCImg*): stage 0 multiplies as 2 subfield + 2 F9 + 4
-//    general per lane instead of 8 general, stage 1 as 4 subfield + 4 F9
-//    instead of 8 F9, and stages 6-9 have lane-uniform elements (the zero ones
-//    are b ^= a only);
-//  * the restricted FFT drops its three multiplies by the zero element
-//    (stage 7 and stage 6's first block at index 0: additive_fft.hpp:129);
-//  * with 72 KB of LDS two workgroups share a CU, so one workgroup's barrier
-//    waits and gather latency run beside the other's transforms (phase stamps
-//    of the 8-wave form: 12% of wave time at its two tile barriers, 14% in the
-//    gather).
-namespace {
-
-constexpr int WW = 4;                       // waves per workgroup
-constexpr int WTHREADS = 64 * WW;
-constexpr int WCOLS = 4 * WW;               // shard columns per tile
-constexpr int WROUNDS = N / WTHREADS;       // gather slots per thread
-constexpr uint32_t WREG0 = kCImgBytes;      // regions after the compact tables
-constexpr uint32_t WSTAGE0 = WREG0 + WW * REG_BYTES;
-constexpr int WLDS_BYTES = int(WSTAGE0 + K * WCOLS * 2);
-static_assert(WLDS_BYTES * 2 <= 160 * 1024, "two workgroups per CU");
-static_assert(kCImgBytes % (16 * WTHREADS) == 0, "whole image chunks per thread");
-
-// 8-B cell of position v in a wave's region: a GF(2)-linear bijection under
-// which the layout A', B' and C reads (32-lane groups) and writes (16-lane
-// groups) are bank-conflict free (scripts/search_raddr.py)
-__host__ __device__ constexpr uint32_t rcell(uint32_t v) {
-  return (((v >> 2) ^ (v >> 4) ^ (v >> 6)) & 1u) | ((((v >> 0) ^ (v >> 5) ^ (v >> 8)) & 1u) << 1) |
-         ((((v >> 1) ^ (v >> 4) ^ (v >> 8)) & 1u) << 2) | ((((v >> 3) ^ (v >> 5) ^ (v >> 7)) & 1u) << 3) |
-         ((((v >> 2) ^ (v >> 8)) & 1u) << 4) | (v & 0x3E0u);
-}
-__host__ __device__ constexpr uint32_t raddr2(uint32_t v) { return rcell(v) << 3; }
-
-// positions of the three layouts: lane part and register part (disjoint bits)
-__host__ __device__ constexpr uint32_t posA2_lane(uint32_t lane) { return lane << 2; }
-__host__ __device__ constexpr uint32_t posA2_reg(int r) { return uint32_t(r & 3) | (uint32_t(r >> 2) << 8); }
-__host__ __device__ constexpr uint32_t posB2_lane(uint32_t lane) { return (lane & 3) | ((lane >> 2) << 6); }
-__host__ __device__ constexpr uint32_t posB2_reg(int r) { return uint32_t(r) << 2; }
-__host__ __device__ constexpr uint32_t posC_lane(uint32_t lane) { return lane; }
-__host__ __device__ constexpr uint32_t posC_reg(int r) { return (uint32_t((r >> 2) & 3) << 6) | (uint32_t(r & 3) << 8); }
-
-// staging of the present data rows y < K for phase 5: 4-row blocks, group g's
-// 8 B of rows 4j..4j+3 contiguous, groups swizzled by the block index
-__device__ __forceinline__ uint32_t stage2_addr(uint32_t y, uint32_t g) {
-  return ((y >> 2) << 7) | ((g ^ ((y >> 2) & 3)) << 5) | ((y & 3) << 3);
-}
-
-__device__ __forceinline__ void load_row_tail32(const uint8_t *row, uint64_t avail, uint32_t (&w)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    w[j] = 0;
-    if (uint64_t(4 * j + 4) <= avail) {
-      w[j] = reinterpret_cast<const uint32_t *>(row)[j];
-    } else if (uint64_t(4 * j) < avail) {
-      for (uint32_t e = 0; 4 * j + e < avail; ++e) w[j] |= uint32_t(row[4 * j + e]) << (8 * e);
-    }
-  }
-}
-
-// IFFT stages 0, 1 in layout A' (r = p0 | p1 << 1 | p8 << 2 | p9 << 3, lane =
-// p2..p7): stage 0 element x = p1 | lane << 1 | p8 << 7 | p9 << 8, kind by
-// (p8, p9): subfield, F9, general, general; stage 1 x = lane | p8 << 6 | p9 << 7:
-// subfield for p9 = 0, F9 for p9 = 1.  The next table is requested before the
-// current butterflies.
-__device__ __forceinline__ void ipassA2(S16 &s, uint32_t lane) {
-  const uint32_t l0 = cimg_lin(lane << 1), l1 = cimg_lin(lane);
-  SubTab s0, s1;
-  F9Tab f0, f1;
-  Tab g0, g1;
-  ctab(l0, cimg_lin(0), s0);
-  ctab(l0, cimg_lin(1), s1);
-  ib(s, 0, 1, s0);
-  ctab(l0, cimg_lin(128), f0);
-  ib(s, 2, 3, s1);
-  ctab(l0, cimg_lin(129), f1);
-  ib(s, 4, 5, f0);
-  ctab(l0, cimg_lin(256), g0);
-  ib(s, 6, 7, f1);
-  ctab(l0, cimg_lin(257), g1);
-  ib(s, 8, 9, g0);
-  ctab(l0, cimg_lin(384), g0);
-  ib(s, 10, 11, g1);
-  ctab(l0, cimg_lin(385), g1);
-  ib(s, 12, 13, g0);
-  ctab(l1, cimg_lin(0), s0);
-  ib(s, 14, 15, g1);
-  ctab(l1, cimg_lin(64), s1);
-  ib(s, 0, 2, s0);
-  ib(s, 1, 3, s0);
-  ctab(l1, cimg_lin(128), f0);
-  ib(s, 4, 6, s1);
-  ib(s, 5, 7, s1);
-  ctab(l1, cimg_lin(192), f1);
-  ib(s, 8, 10, f0);
-  ib(s, 9, 11, f0);
-  ib(s, 12, 14, f1);
-  ib(s, 13, 15, f1);
-}
-
-// IFFT stages 2..5 in layout B' (r = p2..p5, lane = p0 p1 p6..p9): stage 2 + t,
-// block blk: x = blk >> (t + 1) | (lane >> 2) << (3 - t), all subfield
-__device__ __forceinline__ void ipassB2(S16 &s, uint32_t lane) {
-  const uint32_t hl = lane >> 2;
-  const uint32_t L[4] = {cimg_lin(hl << 3), cimg_lin(hl << 2), cimg_lin(hl << 1), cimg_lin(hl)};
-  SubTab U[2];
-  const auto fetch = [&](int t, int blk, int slot) __attribute__((always_inline)) {
-    ctab(L[t], cimg_lin(uint32_t(blk) >> (t + 1)), U[slot]);
-  };
-  fetch(0, 0, 0);
-  int k = 0;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int d = 1 << t;
-#pragma unroll
-    for (int blk = 0; blk < 16; blk += 2 * d, ++k) {
-      const int nt = blk + 2 * d < 16 ? t : t + 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
-      if (nt < 4) fetch(nt, nblk, (k + 1) & 1);
-#pragma unroll
-      for (int i = 0; i < d; ++i) ib(s, blk + i, blk + i + d, U[k & 1]);
-    }
-  }
-}
-
-// IFFT stages 6..9 in layout C (r = p8 | p9 << 1 | p6 << 2 | p7 << 3, lane =
-// p0..p5): the elements are lane-uniform -- stage 6 x = p7 | p8 << 1 | p9 << 2,
-// stage 7 x = p8 | p9 << 1, stage 8 x = p9, stage 9 x = 0 -- and x = 0 is
-// b ^= a only.  The p8 = p9 = 1 registers are not needed past stage 8
-// (positions >= 768 of the IFFT are not read: DESIGN.md §2.5).
-__device__ __forceinline__ void ipassC2(S16 &s) {
-  const auto bx = [&](int a, int b) __attribute__((always_inline)) {
-    s.l[b] ^= s.l[a];
-    s.h[b] ^= s.h[a];
-  };
-  SubTab T[2];
-  // stage 6: pairs (r, r + 4), r in {0..3, 8..11}
-  constexpr int s6[7] = {1, 2, 3, 8, 9, 10, 11};
-  const auto x6 = [](int r) { return uint32_t(((r >> 3) & 1) | ((r & 1) << 1) | (((r >> 1) & 1) << 2)); };
-  ctab(0u, cimg_lin(x6(s6[0])), T[0]);
-  bx(0, 4);
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    if (i + 1 < 7) ctab(0u, cimg_lin(x6(s6[i + 1])), T[(i + 1) & 1]);
-    else ctab(0u, cimg_lin(1), T[(i + 1) & 1]);  // stage 7's first table (x = 1)
-    ib(s, s6[i], s6[i] + 4, T[i & 1]);
-  }
-  // stage 7: pairs (r, r + 8), r = 0..7, x = r & 3 (T[1] holds x = 1)
-  bx(0, 8);
-  bx(4, 12);
-  ctab(0u, cimg_lin(2), T[0]);
-  ib(s, 1, 9, T[1]);
-  ib(s, 5, 13, T[1]);
-  ctab(0u, cimg_lin(3), T[1]);
-  ib(s, 2, 10, T[0]);
-  ib(s, 6, 14, T[0]);
-  ctab(0u, cimg_lin(1), T[0]);  // stage 8
-  ib(s, 3, 11, T[1]);
-  ib(s, 7, 15, T[1]);
-  // stage 8: pairs (r, r + 1), r even: x = p9 (r bit 1)
-#pragma unroll
-  for (int hi = 0; hi < 4; ++hi) {
-    bx(4 * hi, 4 * hi + 1);
-    ib(s, 4 * hi + 2, 4 * hi + 3, T[0]);
-  }
-  // stage 9: pairs (r, r + 2), x = 0; b at p8 = p9 = 1 not needed
-#pragma unroll
-  for (int hi = 0; hi < 4; ++hi) bx(4 * hi, 4 * hi + 2);
-}
-
-}  // namespace
-
-__global__ void __launch_bounds__(WTHREADS, 2) reconstruct_n1024w(
-    const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
-    const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
-    const uint32_t *__restrict__ pattern, const uint32_t *__restrict__ order,
-    uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t batch, DevTables t) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const uint32_t tid0 = threadIdx.x;
-  {  // the compact image (32 KB), every load issued before the first store
-    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
-    constexpr int kPer = int(kCImgBytes / 16 / WTHREADS);
-    v4 v[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) v[k] = reinterpret_cast<const v4 *>(t.cimg)[tid0 + k * WTHREADS];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) reinterpret_cast<v4 *>(lds)[tid0 + k * WTHREADS] = v[k];
-  }
-  __syncthreads();
-
-  const uint64_t ncols = slen / 2;
-  const uint32_t tiles_pp = uint32_t((ncols + WCOLS - 1) / WCOLS);
-  const uint64_t total = uint64_t(tiles_pp) * batch;
-  const uint32_t wave_s = __builtin_amdgcn_readfirstlane(tid0 >> 6);
-  TileWalk walk(blockIdx.x, gridDim.x, tiles_pp);
-  // m[0 .. WROUNDS): this thread's gather slots (gather_order: row << 16 |
-  // mul_index(E[row]), low half 0xFFFF = absent), loaded one tile ahead;
-  // m[WROUNDS], m[WROUNDS + 1]: the output rows y = 4 lane + q (q = 0..3) of
-  // phase 5, 16 bits each: 0xFFFF = present, else mul_index(E[y])
-  constexpr int NM = WROUNDS + 2;
-  auto load_meta = [&](uint64_t bb, uint32_t tid, uint32_t (&m)[NM]) {
-    const uint64_t pt = pattern ? pattern[bb] : bb;
-#pragma unroll
-    for (int r = 0; r < WROUNDS; ++r) m[r] = order[bb * N + r * WTHREADS + tid];
-    const uint32_t y0 = 4 * (tid & 63);
-    const uint32_t p4 = *reinterpret_cast<const uint32_t *>(present + pt * N + y0);
-    const uint2 e4 = *reinterpret_cast<const uint2 *>(elog + pt * N + y0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t e = ((q < 2 ? e4.x : e4.y) >> (16 * (q & 1))) & 0xFFFFu;
-      const uint32_t f = ((p4 >> (8 * q)) & 0xFFu) ? 0xFFFFu : mul_index(e);
-      if (q & 1) m[WROUNDS + (q >> 1)] |= f << 16;
-      else m[WROUNDS + (q >> 1)] = f;
-    }
-  };
-  uint32_t meta[NM], meta_next[NM];
-#pragma unroll
-  for (int i = 0; i < NM; ++i) meta[i] = meta_next[i] = 0;
-  if (blockIdx.x < total) load_meta(walk.b, tid0, meta);
-  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x, walk.advance()) {
-    uint32_t tid = tid0;
-    asm volatile("" : "+v"(tid));
-    const uint32_t lane = tid & 63;
-    const uint64_t b = walk.b, col0 = walk.i * WCOLS;
-    const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
-    uint8_t *O = out + b * ostride;
-    const uint32_t my = WREG0 + wave_s * REG_BYTES;  // this wave's region (absolute LDS address)
-
-    // ---- phase 1: gather + scale this thread's slots' rows (present rows
-    // first; decode_main:174-177) into the 4 groups' regions, absent rows as 0.
-    // The first slot's row and E[v] table are requested before the tile-start
-    // barrier (registers only).
-    const uint64_t avail = slen - 2 * col0;  // bytes of a row inside the tile
-    uint32_t w0[8];
-    Tab RT0;
-    const auto load_row = [&](int r, uint32_t (&w)[8], Tab &RT) __attribute__((always_inline)) {
-      const uint8_t *row = SH + uint64_t(meta[r] >> 16) * sstride + 2 * col0;
-      if (avail >= 32) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const uint4 d = reinterpret_cast<const uint4 *>(row)[q];
-          w[4 * q] = d.x;
-          w[4 * q + 1] = d.y;
-          w[4 * q + 2] = d.z;
-          w[4 * q + 3] = d.w;
-        }
-      } else {  // the payload's last tile
-        load_row_tail32(row, avail, w);
-      }
-      load_tab(t.mtab_tin, meta[r] & 0xffffu, RT);  // scaled into tower coordinates
-    };
-    if ((meta[0] & 0xffffu) != 0xffffu) load_row(0, w0, RT0);
-    lds_barrier();  // the previous tile's readers of the regions are done (LDS only)
-#pragma unroll
-    for (int r = 0; r < WROUNDS; ++r) {
-      const uint32_t v = meta[r] >> 16;
-      uint32_t l[4], h[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) l[g] = h[g] = 0;
-      if ((meta[r] & 0xffffu) != 0xffffu) {
-        uint32_t w1[8];
-        Tab RT1;
-        if (r > 0) load_row(r, w1, RT1);
-        const uint32_t *w = r > 0 ? w1 : w0;
-        const Tab &RT = r > 0 ? RT1 : RT0;
-        if (v < uint32_t(K)) {  // a present data row: kept for phase 5
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-            lds_st2(WSTAGE0 + stage2_addr(v, g), make_uint2(w[2 * g], w[2 * g + 1]));
-        }
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {  // columns 4g..4g+3: words (h0 l0 h1 l1)(h2 l2 h3 l3)
-          const uint32_t a = w[2 * g], c = w[2 * g + 1];
-          const uint32_t xh = vperm(c, a, 0x06040200u), xl = vperm(c, a, 0x07050301u);
-          mul_acc(xl, xh, RT, l[g], h[g]);
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) lds_st2((WREG0 + g * REG_BYTES) | raddr2(v), make_uint2(l[g], h[g]));
-    }
-    if (tile + gridDim.x < total) {
-      uint64_t nb, ni;
-      walk.next_of(nb, ni);
-      load_meta(nb, tid, meta_next);
-    }
-    __syncthreads();
-    const uint64_t cbase = col0 + 4 * uint64_t(wave_s);  // wave-uniform
-    if (cbase >= ncols) {  // a group past the payload's last column: phases 2-5 skipped
-#pragma unroll
-      for (int i = 0; i < NM; ++i) meta[i] = meta_next[i];
-      continue;
-    }
-    // phase-5 tables requested now, consumed after the transform
-    Tab T5[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t m = (meta[WROUNDS + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
-      if (m != 0xFFFFu) load_tab(t.mtab_tout, m, T5[q]);  // tower coordinates in, symbols out
-    }
-
-    // ---- phase 2: IFFT_1024 on this wave's group (inverse_afft, index 0)
-    S16 s;
-    {
-      const uint32_t la = my | raddr2(posA2_lane(lane));
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const uint2 x = lds_ld2(la ^ raddr2(posA2_reg(r)));
-        s.l[r] = x.x;
-        s.h[r] = x.y;
-      }
-      ipassA2(s, lane);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) lds_st2(la ^ raddr2(posA2_reg(r)), make_uint2(s.l[r], s.h[r]));
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
-    {
-      const uint32_t lb = my | raddr2(posB2_lane(lane));
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const uint2 x = lds_ld2(lb ^ raddr2(posB2_reg(r)));
-        s.l[r] = x.x;
-        s.h[r] = x.y;
-      }
-      ipassB2(s, lane);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) lds_st2(lb ^ raddr2(posB2_reg(r)), make_uint2(s.l[r], s.h[r]));
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
-    {
-      const uint32_t lc = my | raddr2(posC_lane(lane));
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const uint2 x = lds_ld2(lc ^ raddr2(posC_reg(r)));
-        s.l[r] = x.x;
-        s.h[r] = x.y;
-      }
-      ipassC2(s);
-    }
-
-    // ---- phases 3 + 4a: formal derivative at y < 256 (poly_encoder.hpp:195-215,
-    // closed form: see reconstruct_n1024 above) and FFT stages 9, 8 (identity
-    // on y < 256)
-    uint32_t ql[4], qh[4];
-    {
-      const uint32_t keep0 = ((lane ^ (lane >> 1)) & 1) ? 0u : 0xffffffffu;
-      const uint32_t m4 = ((lane >> 4) & 1) ? 0u : 0xffffffffu;
-      const uint32_t m5 = ((lane >> 5) & 1) ? 0u : 0xffffffffu;
-      const auto lane_terms = [&](uint32_t c0, uint32_t acc) {
-        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(c0), 0xF5, 0xf, 0xf, false));  // quad [1,1,3,3]
-        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(c0), 0xEE, 0xf, 0xf, false));  // quad [2,3,2,3]
-        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(c0), 0x104, 0xf, 0x5, false));  // row_shl:4, banks 0, 2
-        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(c0), 0x108, 0xf, 0x3, false));  // row_shl:8, banks 0, 1
-        acc = __builtin_amdgcn_bitop3_b32(acc, from_upper(c0, 4), m4, 0x78);  // acc ^ (x & m)
-        acc = __builtin_amdgcn_bitop3_b32(acc, from_upper(c0, 5), m5, 0x78);
-        return __builtin_amdgcn_bitop3_b32(acc, c0, keep0, 0x78);
-      };
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint32_t al = s.l[4 * q + 1] ^ s.l[4 * q + 2], ah = s.h[4 * q + 1] ^ s.h[4 * q + 2];
-        if (!(q & 1)) {  // p6 = 0
-          al ^= s.l[4 * (q | 1)];
-          ah ^= s.h[4 * (q | 1)];
-        }
-        if (!(q & 2)) {  // p7 = 0
-          al ^= s.l[4 * (q | 2)];
-          ah ^= s.h[4 * (q | 2)];
-        }
-        ql[q] = lane_terms(s.l[4 * q], al);
-        qh[q] = lane_terms(s.h[4 * q], ah);
-      }
-    }
-    {
-      // ---- phase 4b: FFT stages 7..0 on y < 256 (afft, additive_fft.hpp:121-141),
-      // element x = y_a >> (m + 1) of the compact image (all subfield).
-      // q bit0 = p6, bit1 = p7; lane bits = p0..p5.
-      auto fb = [&](int a, int bb, const SubTab &T) {
-        mul_acc_sub(ql[bb], qh[bb], T, ql[a], qh[a]);
-        ql[bb] ^= ql[a];
-        qh[bb] ^= qh[a];
-      };
-      auto fx = [&](int a, int bb) {  // element 0: b ^= a only
-        ql[bb] ^= ql[a];
-        qh[bb] ^= qh[a];
-      };
-      const uint32_t l67 = (lane >> 4) & 3, l25 = (lane >> 2) & 15;
-      const uint32_t c5 = cimg_lin(l67), c4 = cimg_lin(l67 << 1), c3 = cimg_lin(l25), c2 = cimg_lin(l25 << 1);
-      const uint32_t c1 = cimg_lin(lane), c0 = cimg_lin(lane << 1);
-      SubTab T[2];
-      ctab(0u, cimg_lin(1), T[0]);  // stage 6, p7 = 1
-      ctab(c5, 0u, T[1]);          // stage 5
-      fx(0, 2);  // stage 7: x = 0
-      fx(1, 3);
-      fx(0, 1);  // stage 6, p7 = 0: x = 0
-      fb(2, 3, T[0]);
-      ctab(c4, 0u, T[0]);  // stage 4, p5 = 0
-      // q (p6, p7) <-> lane bits 4, 5 (p4, p5)
-      swap_bit(ql[0], ql[1], 4, false);
-      swap_bit(qh[0], qh[1], 4, false);
-      swap_bit(ql[2], ql[3], 4, false);
-      swap_bit(qh[2], qh[3], 4, false);
-      swap_bit(ql[0], ql[2], 5, false);
-      swap_bit(qh[0], qh[2], 5, false);
-      swap_bit(ql[1], ql[3], 5, false);
-      swap_bit(qh[1], qh[3], 5, false);
-      // now q = (p4, p5); lane bits 0-3 = p0..p3, 4 = p6, 5 = p7
-      fb(0, 2, T[1]);  // stage 5: x = p6 | p7 << 1
-      fb(1, 3, T[1]);
-      ctab(c4, cimg_lin(1), T[1]);  // stage 4, p5 = 1
-      fb(0, 1, T[0]);  // stage 4: x = p5 | (p6, p7) << 1
-      ctab(c3, 0u, T[0]);  // stage 3
-      fb(2, 3, T[1]);
-      ctab(c2, 0u, T[1]);  // stage 2, p3 = 0
-      // q (p4, p5) <-> lane bits 2, 3 (p2, p3)
-      const bool l2 = (lane >> 2) & 1, l3 = (lane >> 3) & 1;
-      swap_bit(ql[0], ql[1], 2, l2);
-      swap_bit(qh[0], qh[1], 2, l2);
-      swap_bit(ql[2], ql[3], 2, l2);
-      swap_bit(qh[2], qh[3], 2, l2);
-      swap_bit(ql[0], ql[2], 3, l3);
-      swap_bit(qh[0], qh[2], 3, l3);
-      swap_bit(ql[1], ql[3], 3, l3);
-      swap_bit(qh[1], qh[3], 3, l3);
-      // now q = (p2, p3); lane bits 0,1 = p0,p1; 2,3 = p4,p5; 4,5 = p6,p7
-      fb(0, 2, T[0]);  // stage 3: x = p4..p7
-      fb(1, 3, T[0]);
-      ctab(c2, cimg_lin(1), T[0]);  // stage 2, p3 = 1
-      fb(0, 1, T[1]);  // stage 2: x = p3 | p4..p7 << 1
-      ctab(c1, 0u, T[1]);  // stage 1
-      fb(2, 3, T[0]);
-      ctab(c0, 0u, T[0]);  // stage 0, p1 = 0
-      // q (p2, p3) <-> lane bits 0, 1 (p0, p1)
-      const bool l0 = lane & 1, l1 = (lane >> 1) & 1;
-      swap_bit(ql[0], ql[1], 0, l0);
-      swap_bit(qh[0], qh[1], 0, l0);
-      swap_bit(ql[2], ql[3], 0, l0);
-      swap_bit(qh[2], qh[3], 0, l0);
-      swap_bit(ql[0], ql[2], 1, l1);
-      swap_bit(qh[0], qh[2], 1, l1);
-      swap_bit(ql[1], ql[3], 1, l1);
-      swap_bit(qh[1], qh[3], 1, l1);
-      // now q = (p0, p1); lane = (p2 .. p7): y = 4 * lane + q
-      fb(0, 2, T[1]);  // stage 1: x = p2..p7
-      fb(1, 3, T[1]);
-      ctab(c0, cimg_lin(1), T[1]);  // stage 0, p1 = 1
-      fb(0, 1, T[0]);  // stage 0: x = p1 | p2..p7 << 1
-      fb(2, 3, T[1]);
-    }
-
-    // ---- phase 5: y = 4 lane + q; columns cbase + c (decode_main:185-188,
-    // reconstructSub:138-149)
-    {
-      uint32_t ra[4], rc[4];  // rows 4 lane .. + 3 of group `wave`, as received
-      {
-        uint32_t ol2 = lane;
-        asm volatile("" : "+v"(ol2));
-        const uint32_t sa = WSTAGE0 + stage2_addr(4 * ol2, wave_s);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint2 d = lds_ld2(sa + 8 * q);
-          ra[q] = d.x;
-          rc[q] = d.y;
-        }
-      }
-      uint32_t ol[4], oh[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t m = (meta[WROUNDS + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
-        ol[q] = oh[q] = 0;
-        if (m != 0xFFFFu) {
-          mul_acc(ql[q], qh[q], T5[q], ol[q], oh[q]);
-        } else {
-          oh[q] = vperm(rc[q], ra[q], 0x06040200u);
-          ol[q] = vperm(rc[q], ra[q], 0x07050301u);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {  // column c of the group: 4 consecutive y -> 8 bytes BE
-        const uint64_t col = cbase + c;
-        if (col >= ncols) break;
-        const uint32_t w0 = vperm(ol[0], oh[0], 0x0c0c0400u + 0x0101u * c) |
-                            (vperm(ol[1], oh[1], 0x0c0c0400u + 0x0101u * c) << 16);
-        const uint32_t w1 = vperm(ol[2], oh[2], 0x0c0c0400u + 0x0101u * c) |
-                            (vperm(ol[3], oh[3], 0x0c0c0400u + 0x0101u * c) << 16);
-        *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NM; ++i) meta[i] = meta_next[i];
-  }
-}
-
-hipError_t launch_reconstruct_n1024w(const CodeParams &p, const DevTables &t, const uint8_t *d_shards,
-                                     size_t slen, size_t sstride, const uint8_t *d_present,
-                                     const uint16_t *d_err_log, const uint32_t *d_pattern, size_t batch,
-                                     uint8_t *d_out, size_t ostride, void *scratch, hipStream_t s) {
-  int cus = 0;
-  if (!scratch || !t.cimg) return hipErrorInvalidValue;
-  if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&reconstruct_n1024w), WLDS_BYTES, &cus);
-      e != hipSuccess)
-    return e;
-  uint32_t *order = static_cast<uint32_t *>(scratch);  // gather_order_bytes(p, batch)
-  if (const hipError_t e = launch_gather_order(p, d_present, d_err_log, d_pattern, batch, order, s); e != hipSuccess)
-    return e;
-  const size_t tiles = (slen / 2 + WCOLS - 1) / WCOLS * batch;
-  const size_t slots = 2 * size_t(cus);  // two workgroups per CU
-  const unsigned grid = unsigned(tiles < slots ? tiles : slots);
-  hipLaunchKernelGGL(reconstruct_n1024w, dim3(grid), dim3(WTHREADS), WLDS_BYTES, s, d_shards, uint64_t(slen),
-                     uint64_t(sstride), d_present, d_err_log, d_pattern, order, d_out, uint64_t(ostride),
-                     int(p.nv), uint32_t(batch), t);
-  return hipGetLastError();
-}
-
 bool n1024_applicable(const CodeParams &p) { return p.n == 1024 && p.k == 256; }
 
 // packed tiles: fewer columns per payload than a tile, or a shard pitch / base
@@ -1335,9 +818,6 @@ hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
     return e && e[0] == '1';
   }();
   const bool packed = force_packed || n1024_packed(slen, reinterpret_cast<uintptr_t>(d_shards), sstride);
-  if (!packed)
-    return launch_reconstruct_n1024w(p, t, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch, d_out,
-                                      ostride, scratch, s);
   const size_t ncols4 = (slen / 2 + 3) / 4 * 4;
   if (packed && (reinterpret_cast<uintptr_t>(d_shards) % 2 != 0 || sstride % 2 != 0 ||
                  ncols4 * batch + COLS >= (size_t(1) << 32)))

@@ -73,8 +73,35 @@ elif kind == "dec":
     s = rep(s, "    __builtin_amdgcn_s_setprio(0);  // the next tile's gather: equal\n  }\n",
             "    __builtin_amdgcn_s_setprio(0);  // the next tile's gather: equal\n    STAMP(4);\n  }\n" + FLUSH)
     names = ["gather", "barriers", "ifft", "deriv+fft", "output"]
+elif kind == "encw":
+    s = open(f"{ROOT}/erasure-coding-crust_amd/csrc/enc_k256w.hip").read()
+    s = rep(s, "namespace ecamd {\nnamespace {", "namespace ecamd {\n__device__ unsigned long long g_stamp[16];\nnamespace {")
+    s = rep(s, "  __syncthreads();\n\n  const uint64_t npieces", "  __syncthreads();\n" + STAMP + "\n  const uint64_t npieces")
+    s = rep(s, "    const auto rsync = [&]() __attribute__((always_inline)) { lds_barrier(); };",
+            "    const auto rsync = [&]() __attribute__((always_inline)) { STAMP(3); lds_barrier(); STAMP(1); };")
+    s = rep(s, "      __builtin_amdgcn_s_setprio(1);\n", "      STAMP(3);\n      __builtin_amdgcn_s_setprio(1);\n")
+    s = rep(s, "      __builtin_amdgcn_s_setprio(0);\n    };", "      __builtin_amdgcn_s_setprio(0);\n      STAMP(2);\n    };")
+    s = rep(s, "    // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)\n",
+            "    STAMP(0);\n    // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)\n")
+    s = rep(s, "  }\n}\n\nhipError_t launch_encode_k256w", "  }\n" + FLUSH + "}\n\nhipError_t launch_encode_k256w")
+    names = ["load", "barrier", "stores", "compute"]
+elif kind == "decw":
+    s = open(f"{ROOT}/erasure-coding-crust_amd/csrc/dec_n1024.hip").read()
+    s = rep(s, "namespace ecamd {\nnamespace {", "namespace ecamd {\n__device__ unsigned long long g_stamp[16];\nnamespace {")
+    i = s.index("reconstruct_n1024w(")
+    head, tail = s[:i], s[i:]
+    tail = rep(tail, "  __syncthreads();\n\n  const uint64_t ncols", "  __syncthreads();\n" + STAMP + "\n  const uint64_t ncols")
+    tail = rep(tail, "    if ((meta[0] & 0xffffu) != 0xffffu) load_row(0, w0, RT0);\n    lds_barrier();",
+               "    if ((meta[0] & 0xffffu) != 0xffffu) load_row(0, w0, RT0);\n    STAMP(0);\n    lds_barrier();\n    STAMP(1);")
+    tail = rep(tail, "    __syncthreads();\n    const uint64_t cbase", "    STAMP(0);\n    __syncthreads();\n    STAMP(1);\n    const uint64_t cbase")
+    tail = rep(tail, "    // ---- phases 3 + 4a", "    STAMP(2);\n    // ---- phases 3 + 4a")
+    tail = rep(tail, "    // ---- phase 5: y = 4 lane + q", "    STAMP(3);\n    // ---- phase 5: y = 4 lane + q")
+    tail = rep(tail, "    for (int i = 0; i < NM; ++i) meta[i] = meta_next[i];\n    __builtin_amdgcn_s_setprio(0);  // the next tile's gather: equal\n  }\n}",
+               "    for (int i = 0; i < NM; ++i) meta[i] = meta_next[i];\n    __builtin_amdgcn_s_setprio(0);\n    STAMP(4);\n  }\n" + FLUSH + "}")
+    s = head + tail
+    names = ["gather", "barriers", "ifft", "deriv+fft", "output"]
 else:
-    sys.exit("kind: enc | dec")
+    sys.exit("kind: enc | dec | encw | decw")
 s += READER.replace('namespace ecamd {\n__device__ unsigned long long g_stamp[16];\n}\n', '')
 open(out, "w").write(s)
 print(",".join(names))
