@@ -460,6 +460,8 @@ def main():
                          "n_validators=nv and report them in `sizes`; 'none': skip; or a comma list")
     ap.add_argument("--sweep-cpu-seconds", type=float, default=0.5,
                     help="ec-cpp sample per size and thread count in the sweep")
+    ap.add_argument("--row-stride", type=int, default=0,
+                    help="device shard row stride in bytes (0: shard_len rounded up to --row-align)")
     ap.add_argument("--row-align", type=int, default=64,
                     help="device shard row stride = shard_len rounded up to this many bytes")
     ap.add_argument("--graph", action="store_true",
@@ -500,6 +502,10 @@ def main():
     cnt = {"threshold": thr, "k": k}.get(args.present) or int(args.present)
     sl = E.shard_len(nv, plen)
     ss = (sl + args.row_align - 1) // args.row_align * args.row_align  # device shard row stride
+    if args.row_stride:
+        if args.row_stride < sl or args.row_stride % 16:
+            ap.error(f"--row-stride must be >= shard_len ({sl}) and a multiple of 16")
+        ss = args.row_stride
     dev = torch.device("cuda", local)
 
     # synthetic inputs, resident before timing; seeds are global payload indices

@@ -30,7 +30,7 @@ thr = (NV - 1) // 3 + 1
 K = 1 << (thr.bit_length() - 1)
 SL = ((P + 2 * K - 1) // (2 * K)) * 2
 KERNELS = {"encode_k256": "encode", "reconstruct_n1024": "reconstruct",
-           "encode_k1024": "encode", "reconstruct_n4096": "reconstruct",
+           "encode_k1024_fused": "encode", "reconstruct_n4096": "reconstruct",
            "encode_gen": "encode", "reconstruct_gen": "reconstruct",
            "encode_g": "encode", "reconstruct_g": "reconstruct", "error_locator_g": "error_locator"}
 

@@ -13,7 +13,7 @@ import synth  # noqa: E402
 
 kind, names = sys.argv[1], sys.argv[2].split(",")
 B = int(sys.argv[3]) if len(sys.argv) > 3 else 1024
-nv, plen = 1024, 1_000_000
+nv, plen = int(os.environ.get("NV", "1024")), 1_000_000
 n, k, thr = E.code_params(nv)
 sl = E.shard_len(nv, plen)
 ss = (sl + 63) // 64 * 64

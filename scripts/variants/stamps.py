@@ -28,14 +28,14 @@ extern "C" int ECCR_DIAG_stamps(unsigned long long *out, int n, int reset) {
 }
 '''
 DECL = ('namespace ecamd {\n__device__ unsigned long long g_stamp[16];\n}\n')
-STAMP = ('  uint64_t st_last_ = __builtin_amdgcn_s_memtime(), acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};\n'
+STAMP = ('  uint64_t st_last_ = __builtin_amdgcn_s_memtime(), acc_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};\n'
          '  const auto STAMP = [&](int i) __attribute__((always_inline)) {\n'
          '    const uint64_t now_ = __builtin_amdgcn_s_memtime();\n'
          '    acc_[i] += now_ - st_last_;\n'
          '    st_last_ = now_;\n'
          '  };\n')
 FLUSH = ('  if ((threadIdx.x & 63) == 0)\n'
-         '    for (int i = 0; i < 8; ++i) atomicAdd(&g_stamp[i], (unsigned long long)acc_[i]);\n')
+         '    for (int i = 0; i < 12; ++i) atomicAdd(&g_stamp[i], (unsigned long long)acc_[i]);\n')
 
 
 def rep(s, old, new, count=1):
@@ -100,8 +100,67 @@ elif kind == "decw":
                "    for (int i = 0; i < NM; ++i) meta[i] = meta_next[i];\n    __builtin_amdgcn_s_setprio(0);\n    STAMP(4);\n  }\n" + FLUSH + "}")
     s = head + tail
     names = ["gather", "barriers", "ifft", "deriv+fft", "output"]
+elif kind == "enc4":
+    s = open(f"{ROOT}/erasure-coding-crust_amd/csrc/enc_k1024.hip").read()
+    s = rep(s, "namespace ecamd {\nnamespace {", "namespace ecamd {\n__device__ unsigned long long g_stamp[16];\nnamespace {")
+    s = rep(s, "  Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);  // index 0 (the IFFT)\n  __syncthreads();\n",
+            "  Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);  // index 0 (the IFFT)\n  __syncthreads();\n" + STAMP)
+    s = rep(s, "    // systematic shards 0..1023 = the data symbols (poly_encoder.hpp:239)\n",
+            "    STAMP(0);\n    // systematic shards 0..1023 = the data symbols (poly_encoder.hpp:239)\n")
+    s = rep(s, "    // the index-0 tables (the last tile's DMA) landed; the regions are free\n",
+            "    STAMP(1);\n    // the index-0 tables (the last tile's DMA) landed; the regions are free\n")
+    s = rep(s, "    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    lds_barrier();\n    if (!idle) {\n      to_tower(g0, g1);",
+            "    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    lds_barrier();\n    STAMP(2);\n    if (!idle) {\n      to_tower(g0, g1);")
+    s = rep(s, "    lds_barrier();  // every wave is done with the index-0 tables\n",
+            "    STAMP(3);\n    lds_barrier();  // every wave is done with the index-0 tables\n")
+    s = rep(s, "      asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // coset s's tables and coefficients landed\n      lds_barrier();  // (all waves' slices) and the regions are free\n",
+            "      STAMP(4);\n      asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // coset s's tables and coefficients landed\n      lds_barrier();  // (all waves' slices) and the regions are free\n      STAMP(2);\n")
+    s = rep(s, "        to_tower(g0, g1);  // back to symbol coordinates\n      }\n",
+            "        to_tower(g0, g1);  // back to symbol coordinates\n      }\n      STAMP(5);\n")
+    s = rep(s, """      for (uint32_t hf = 0; hf < 2; ++hf) {
+        if (hf) lds_barrier();
+        if (!idle) stage_half(g0, g1, my, lane, wave, hf);
+        lds_barrier();
+        if (hf == 0)  // every wave is past its FFT: the next set (index 0 after the last coset)
+          Tabs::dma_image<THREADS>(tabs, t.timg_t + (s + 1 < ncos ? s + 1 : 0) * kTabImageBytes, tid);
+        store_half(regions, SH, sstride, s * K + 512 * hf, nv, piece0, npieces, wave, lane);
+      }""", """      for (uint32_t hf = 0; hf < 2; ++hf) {
+        if (hf) lds_barrier();
+        STAMP(7);
+        if (!idle) stage_half(g0, g1, my, lane, wave, hf);
+        STAMP(8);
+        lds_barrier();
+        STAMP(7);
+        if (hf == 0)  // every wave is past its FFT: the next set (index 0 after the last coset)
+          Tabs::dma_image<THREADS>(tabs, t.timg_t + (s + 1 < ncos ? s + 1 : 0) * kTabImageBytes, tid);
+        STAMP(9);
+        store_half(regions, SH, sstride, s * K + 512 * hf, nv, piece0, npieces, wave, lane);
+        STAMP(10);
+      }""")
+    s = rep(s, "    if (ncos > 3) coset(std::integral_constant<uint32_t, 3>());\n  }\n",
+            "    if (ncos > 3) coset(std::integral_constant<uint32_t, 3>());\n    STAMP(1);\n  }\n" + FLUSH)
+    names = ["load", "sys+stage+stores", "vmcnt0+barrier", "ifft", "coef+barrier", "fft", "-", "barriers", "stage", "dma", "stores"]
+elif kind == "dec4":
+    s = open(f"{ROOT}/erasure-coding-crust_amd/csrc/dec_n4096.hip").read()
+    s = rep(s, "namespace ecamd {\nnamespace {", "namespace ecamd {\n__device__ unsigned long long g_stamp[16];\nnamespace {")
+    s = rep(s, "  const uint64_t ncols = slen / 2;\n  const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);\n",
+            STAMP + "  const uint64_t ncols = slen / 2;\n  const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);\n")
+    s = rep(s, "      if (qnext >= 0) load_meta(qnext, tq);\n      asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // table image landed\n      lds_barrier();\n",
+            "      if (qnext >= 0) load_meta(qnext, tq);\n      STAMP(0);\n      asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // table image landed\n      lds_barrier();\n      STAMP(1);\n")
+    s = rep(s, "        ifft1024<q == 0, tower_sub_min(q)>(Qq, tabs, my, lq);\n      }\n",
+            "        ifft1024<q == 0, tower_sub_min(q)>(Qq, tabs, my, lq);\n      }\n      STAMP(2);\n")
+    s = rep(s, "        Tabs::dma_image<THREADS>(tabs, t.timg_t + qnext * kTabImageBytes, tq);\n        __builtin_amdgcn_sched_barrier(0);\n      }\n",
+            "        Tabs::dma_image<THREADS>(tabs, t.timg_t + qnext * kTabImageBytes, tq);\n        __builtin_amdgcn_sched_barrier(0);\n      }\n      STAMP(3);\n")
+    s = rep(s, "        asm volatile(\"\" : \"+v\"(P.l[r]), \"+v\"(P.h[r]), \"+v\"(Qa.l[r]), \"+v\"(Qa.h[r]));\n      __builtin_amdgcn_sched_barrier(0);\n    };",
+            "        asm volatile(\"\" : \"+v\"(P.l[r]), \"+v\"(P.h[r]), \"+v\"(Qa.l[r]), \"+v\"(Qa.h[r]));\n      __builtin_amdgcn_sched_barrier(0);\n      STAMP(4);\n    };")
+    s = rep(s, "    const uint64_t cbase = col0 + 4 * wave;\n    lds_barrier();  // every wave is done with the FFT tables\n",
+            "    const uint64_t cbase = col0 + 4 * wave;\n    STAMP(5);\n    lds_barrier();  // every wave is done with the FFT tables\n")
+    s = rep(s, "    lds_barrier();\n    if (idle) continue;\n", "    lds_barrier();\n    STAMP(6);\n    if (idle) continue;\n")
+    s = rep(s, "        reinterpret_cast<uint4 *>(dst)[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);\n      }\n    }\n  }\n}",
+            "        reinterpret_cast<uint4 *>(dst)[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);\n      }\n    }\n    STAMP(7);\n  }\n" + FLUSH + "}")
+    names = ["gather", "wait_tab+bar", "ifft", "bar+dma", "accum", "deriv+fft", "outtab", "output"]
 else:
-    sys.exit("kind: enc | dec | encw | decw")
+    sys.exit("kind: enc | dec | encw | decw | enc4 | dec4")
 s += READER.replace('namespace ecamd {\n__device__ unsigned long long g_stamp[16];\n}\n', '')
 open(out, "w").write(s)
 print(",".join(names))
