@@ -215,8 +215,12 @@ __global__ void __launch_bounds__(THREADS)
       lds_barrier();
       store_half(regions, SH, sstride, 512 * hf, nv, piece0, npieces, wave, lane);
     }
-    // the index-0 tables (the last tile's DMA) landed; the regions are free
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the index-0 tables (the last tile's DMA, issued before the 16 fast-form
+    // systematic stores just made) landed; the regions are free
+    if (((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0 && piece0 + TILE <= npieces)
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
     if (!idle) {
       to_tower(g0, g1);
@@ -231,10 +235,11 @@ __global__ void __launch_bounds__(THREADS)
     lds_barrier();  // every wave is done with the index-0 tables
     Tabs::dma_image<THREADS>(tabs, t.timg_t + kTabImageBytes, tid);
     // cs: std::integral_constant coset number (its image's subfield stages)
+    const bool fast_rows = ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0 && piece0 + TILE <= npieces;
     const auto coset = [&](auto cs) __attribute__((always_inline)) {
       constexpr uint32_t s = decltype(cs)::value;
-      if (s > 1 && !idle) load_coef();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // coset s's tables and coefficients landed
+      if (s > 1 && fast_rows && int(s * K) <= nv) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // coset s's tables and coefficients landed
       lds_barrier();  // (all waves' slices) and the regions are free
       if (!idle) {
         fft1024<false, tower_sub_min(int(s))>(g0, tabs, my, lane);
@@ -248,6 +253,7 @@ __global__ void __launch_bounds__(THREADS)
         lds_barrier();
         if (hf == 0)  // every wave is past its FFT: the next set (index 0 after the last coset)
           Tabs::dma_image<THREADS>(tabs, t.timg_t + (s + 1 < ncos ? s + 1 : 0) * kTabImageBytes, tid);
+        if (hf == 1 && s + 1 < ncos && !idle) load_coef();  // g0 / g1 are staged
         store_half(regions, SH, sstride, s * K + 512 * hf, nv, piece0, npieces, wave, lane);
       }
     };
