@@ -94,17 +94,31 @@ Lin n4096_lin(int nq) {
 // reconstruct fills its output tables with one linear LDS-DMA per tile
 // instead of a per-tile gather of 1024 indexed 80-byte tables (two dependent
 // global latencies).  Chunk i of the image is plane i / 1024, slot i % 1024 of
-// entry y = (slot & ~15) | f with LdsTabs::addr's swizzle f inverted.
+// entry y = (slot & ~15) | f with LdsTabs::addr's swizzle f inverted.  After
+// the image, the payload's present mask of y < 1024 (bit y of dword y / 32: row
+// y is received), read by the reconstruct at its tile start so that the output
+// phase's received-row loads can be issued before the final FFT.
+constexpr size_t kOutImageBytes = kTabImageBytes + 1024 / 8;
 __global__ void __launch_bounds__(256)
-    n4096_out_image(const uint16_t *__restrict__ elog, const uint32_t *__restrict__ pattern, int n,
+    n4096_out_image(const uint16_t *__restrict__ elog, const uint8_t *__restrict__ present,
+                    const uint32_t *__restrict__ pattern, int n, int nv,
                     const MulTab *__restrict__ mtab, uint8_t *__restrict__ img) {
-  const uint64_t b = blockIdx.x;
-  const uint16_t *E = elog + (pattern ? pattern[b] : b) * uint64_t(n);
-  uint4 *dst = reinterpret_cast<uint4 *>(img + b * kTabImageBytes);
+  const uint64_t b = blockIdx.x, pt = pattern ? pattern[b] : b;
+  const uint16_t *E = elog + pt * uint64_t(n);
+  uint4 *dst = reinterpret_cast<uint4 *>(img + b * kOutImageBytes);
   for (uint32_t i = threadIdx.x; i < 5 * 1024; i += 256) {
     const uint32_t q = i >> 10, sl = i & 1023;
     const uint32_t y = (sl & ~15u) | ((sl ^ (sl >> 4) ^ (sl >> 8)) & 15u);
     dst[i] = reinterpret_cast<const uint4 *>(mtab + mul_index(E[y]))[q];
+  }
+  if (threadIdx.x < 32) {
+    const uint8_t *pr = present + pt * uint64_t(n);
+    uint32_t m = 0;
+    for (uint32_t j = 0; j < 32; ++j) {
+      const uint32_t y = 32 * threadIdx.x + j;
+      m |= uint32_t(int(y) < nv && pr[y]) << j;
+    }
+    reinterpret_cast<uint32_t *>(img + b * kOutImageBytes + kTabImageBytes)[threadIdx.x] = m;
   }
 }
 
@@ -140,6 +154,15 @@ reconstruct_n4096(
     const uint8_t *pr = present + pt * N;
     const uint16_t *E = elog + pt * N;
     uint8_t *O = out + b * ostride;
+    // k = 1024 (n4096_out_image's mask): bit r of pm = row 16 lane + r received;
+    // bit i of pw[j] = row 128 wave + 32 j + i received (wave-uniform)
+    uint32_t pm = 0;
+    uint4 pw = make_uint4(0, 0, 0, 0);
+    if constexpr (KB == 10) {
+      const uint32_t *mask = reinterpret_cast<const uint32_t *>(oimg + b * kOutImageBytes + kTabImageBytes);
+      pm = mask[lane >> 1] >> (16 * (lane & 1));
+      pw = reinterpret_cast<const uint4 *>(mask)[wave];
+    }
     S16 P, Qa;  // the two accumulators of the linearised cross-quarter stages
     // a wave whose 4 columns lie past the payload's last one (its last, partial
     // tile: 1 MB at k = 1024 is 489 columns, the 16th tile has 9) gathers with
@@ -312,6 +335,8 @@ reconstruct_n4096(
     // lane = p0..p5, r = (p8, p9, p6, p7).
     __builtin_amdgcn_s_setprio(0);
     S16 Y;
+    const uint64_t cbase = col0 + 4 * wave;
+    const bool full = cbase + 4 <= ncols;
     if (!idle) {
       derivative<LC, 10, KB>(P, lane);  // at the registers reaching y < k only
 #pragma unroll
@@ -331,11 +356,26 @@ reconstruct_n4096(
 
     // ---- output (decode_main:185-188, reconstructSub:138-149): erased y < k
     // scaled by E[y] (tables now in LDS), present y copied from the shard
-    const uint64_t cbase = col0 + 4 * wave;
     lds_barrier();  // every wave is done with the FFT tables
     if constexpr (KB == 10) {  // all 1024, from this payload's prebuilt image (n4096_out_image)
       __builtin_amdgcn_sched_barrier(0);
-      Tabs::dma_image<THREADS>(tabs, oimg + b * kTabImageBytes, tid);
+      Tabs::dma_image<THREADS>(tabs, oimg + b * kOutImageBytes, tid);
+      if (col0 + COLS <= ncols) {
+        // the received rows' 64-B tile segments -> the regions, by LDS-DMA in the
+        // same latency: 1 KB window w = rows 16 w .. 16 w + 15, 16-B slot
+        // (4 (y & 15) + chunk) ^ (w & 15) (swizzled so that the reads below,
+        // one row per lane, spread over the banks); each wave fills 8 windows
+        const uint32_t pws[4] = {pw.x, pw.y, pw.z, pw.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t W = 8 * wave + j, l = lane ^ (W & 15);
+          const uint32_t yy = l >> 2;
+          if ((pws[j >> 1] >> (16 * (j & 1) + yy)) & 1)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(SH + uint64_t(16 * W + yy) * sstride + 2 * col0 + 16 * (l & 3)),
+                (__attribute__((address_space(3))) void *)(regions + 1024 * W), 16, 0, 0);
+        }
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     } else  // k = 256 / 512: the erased y < k only (nv = 2500 3.32 -> 3.20 ms per 512 x 1 MB)
@@ -348,7 +388,6 @@ reconstruct_n4096(
       constexpr int SB = swap_rbit<LC>();
       uint32_t olane = lane;
       asm volatile("" : "+v"(olane));
-      const bool full = cbase + 4 <= ncols;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         if (((r >> SB) & 1) || !live_above<LC, 10, KB>(r & ~(1 << SB), KB - 1)) continue;
@@ -394,10 +433,15 @@ reconstruct_n4096(
       for (int r = 0; r < 16; ++r) {
         const uint32_t y = 16 * lane + r;
         ol[r] = oh[r] = 0;
-        if (int(y) < nv && pr[y]) {
+        if ((pm >> r) & 1) {  // int(y) < nv && pr[y]
           const uint8_t *row = SH + uint64_t(y) * sstride + 2 * cbase;
           uint32_t a = 0, c = 0;
-          if (cbase + 4 <= ncols) {
+          if (col0 + COLS <= ncols) {  // staged above
+            const uint2 d = lds_ld2(lds_addr(regions) + 1024 * lane + 16 * ((4 * r + (wave >> 1)) ^ (lane & 15)) +
+                                    8 * (wave & 1));
+            a = d.x;
+            c = d.y;
+          } else if (full) {
             const uint2 d = *reinterpret_cast<const uint2 *>(row);
             a = d.x;
             c = d.y;
@@ -434,7 +478,7 @@ reconstruct_n4096(
 }
 
 size_t n4096_scratch_bytes(const CodeParams &p, size_t batch) {
-  return gather_order_bytes(p, batch) + (p.k == 1024 ? batch * kTabImageBytes : 0);
+  return gather_order_bytes(p, batch) + (p.k == 1024 ? batch * kOutImageBytes : 0);
 }
 
 bool n4096_applicable(const CodeParams &p) {  // the (n, k) instantiated below
@@ -461,8 +505,8 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
     return e;
   uint8_t *oimg = static_cast<uint8_t *>(scratch) + gather_order_bytes(p, batch);
   if (p.k == 1024)
-    hipLaunchKernelGGL(n4096_out_image, dim3(unsigned(batch)), dim3(256), 0, s, d_err_log, d_pattern,
-                       int(p.n), t.mtab_tout, oimg);  // tower in, symbols out
+    hipLaunchKernelGGL(n4096_out_image, dim3(unsigned(batch)), dim3(256), 0, s, d_err_log, d_present, d_pattern,
+                       int(p.n), int(p.nv), t.mtab_tout, oimg);  // tower in, symbols out
   const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   static const Lin lin4 = n4096_lin(4), lin2 = n4096_lin(2);
