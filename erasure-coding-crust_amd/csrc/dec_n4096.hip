@@ -124,6 +124,14 @@ __global__ void __launch_bounds__(256)
 
 }  // namespace
 
+// layout C after the restricted FFT: y0 = (lane << 1) | reg_pos(r, swap bit),
+// the register part only in y bits 7.. (the output's mask dword md[R >> 7])
+constexpr bool regbits_above_lane() {
+  for (int r = 0; r < 16; ++r)
+    if (reg_pos<LC, 10>(r, swap_rbit<LC>()) & 127u) return false;
+  return true;
+}
+
 // NQ = n / 1024 quarters (2 or 4); K = k = 2^KB (256, 512 or 1024)
 template <int NQ, int KB>
 __global__ void __launch_bounds__(THREADS)
@@ -133,7 +141,6 @@ reconstruct_n4096(
     const uint32_t *__restrict__ pattern, const uint32_t *__restrict__ order,
     uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t K, uint32_t batch,
     DevTables t, Lin lin, const uint8_t *__restrict__ oimg) {
-  constexpr int N = 1024 * NQ;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
   uint8_t *regions = lds + Tabs::kBytes;
@@ -150,19 +157,17 @@ reconstruct_n4096(
     const uint64_t b = tile / tiles_pp;
     const uint64_t col0 = (tile % tiles_pp) * COLS;
     const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
-    const uint64_t pt = pattern ? pattern[b] : b;  // erasure pattern of payload b
-    const uint8_t *pr = present + pt * N;
-    const uint16_t *E = elog + pt * N;
     uint8_t *O = out + b * ostride;
-    // k = 1024 (n4096_out_image's mask): bit r of pm = row 16 lane + r received;
-    // bit i of pw[j] = row 128 wave + 32 j + i received (wave-uniform)
+    // n4096_out_image's mask of the received rows y < k: bit i of pw[j] = row
+    // (k / 8) wave + 32 j + i (wave-uniform, for the staging DMA); k = 1024: bit r
+    // of pm = row 16 lane + r (the output rows of the lane)
+    const uint32_t *mask = reinterpret_cast<const uint32_t *>(oimg + b * kOutImageBytes + kTabImageBytes);
+    constexpr int MPW = (1 << KB) / 256;  // mask dwords per wave
+    uint32_t pw[MPW];
+#pragma unroll
+    for (int j = 0; j < MPW; ++j) pw[j] = mask[MPW * wave + j];
     uint32_t pm = 0;
-    uint4 pw = make_uint4(0, 0, 0, 0);
-    if constexpr (KB == 10) {
-      const uint32_t *mask = reinterpret_cast<const uint32_t *>(oimg + b * kOutImageBytes + kTabImageBytes);
-      pm = mask[lane >> 1] >> (16 * (lane & 1));
-      pw = reinterpret_cast<const uint4 *>(mask)[wave];
-    }
+    if constexpr (KB == 10) pm = mask[lane >> 1] >> (16 * (lane & 1));
     S16 P, Qa;  // the two accumulators of the linearised cross-quarter stages
     // a wave whose 4 columns lie past the payload's last one (its last, partial
     // tile: 1 MB at k = 1024 is 489 columns, the 16th tile has 9) gathers with
@@ -357,54 +362,65 @@ reconstruct_n4096(
     // ---- output (decode_main:185-188, reconstructSub:138-149): erased y < k
     // scaled by E[y] (tables now in LDS), present y copied from the shard
     lds_barrier();  // every wave is done with the FFT tables
-    if constexpr (KB == 10) {  // all 1024, from this payload's prebuilt image (n4096_out_image)
-      __builtin_amdgcn_sched_barrier(0);
-      Tabs::dma_image<THREADS>(tabs, oimg + b * kOutImageBytes, tid);
-      if (col0 + COLS <= ncols) {
-        // the received rows' 64-B tile segments -> the regions, by LDS-DMA in the
-        // same latency: 1 KB window w = rows 16 w .. 16 w + 15, 16-B slot
-        // (4 (y & 15) + chunk) ^ (w & 15) (swizzled so that the reads below,
-        // one row per lane, spread over the banks); each wave fills 8 windows
-        const uint32_t pws[4] = {pw.x, pw.y, pw.z, pw.w};
+    // the output tables E[y] from this payload's prebuilt image (n4096_out_image)
+    __builtin_amdgcn_sched_barrier(0);
+    Tabs::dma_image<THREADS>(tabs, oimg + b * kOutImageBytes, tid);
+    const bool staged = col0 + COLS <= ncols;  // the received rows y < k go through the regions
+    if (staged) {
+      // their 64-B tile segments -> the regions, by LDS-DMA in the same latency:
+      // 1 KB window w = rows 16 w .. 16 w + 15, 16-B slot (4 (y & 15) + chunk) ^
+      // (w & 15) (swizzled so that the reads below, one row per lane, spread
+      // over the banks); each wave fills k / 128 windows
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint32_t W = 8 * wave + j, l = lane ^ (W & 15);
-          const uint32_t yy = l >> 2;
-          if ((pws[j >> 1] >> (16 * (j & 1) + yy)) & 1)
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)(SH + uint64_t(16 * W + yy) * sstride + 2 * col0 + 16 * (l & 3)),
-                (__attribute__((address_space(3))) void *)(regions + 1024 * W), 16, 0, 0);
-        }
+      for (int j = 0; j < 2 * MPW; ++j) {
+        const uint32_t W = 2 * MPW * wave + j, l = lane ^ (W & 15);
+        const uint32_t yy = l >> 2;
+        if ((pw[j >> 1] >> (16 * (j & 1) + yy)) & 1)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void *)(SH + uint64_t(16 * W + yy) * sstride + 2 * col0 + 16 * (l & 3)),
+              (__attribute__((address_space(3))) void *)(regions + 1024 * W), 16, 0, 0);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    } else  // k = 256 / 512: the erased y < k only (nv = 2500 3.32 -> 3.20 ms per 512 x 1 MB)
-      Tabs::gather_if<THREADS>(
-          tabs, t.mtab_tout, [&](uint32_t y) { return mul_index(E[y]); },  // tower in, symbols out
-          [&](uint32_t y) { return y < K; }, [&](uint32_t y) { return !(int(y) < nv && pr[y]); }, tid);
+    }
+    // k < 1024: mask dwords (lane >> 4) + 4 m (rows y0 = 2 lane + 128 m + (0, 1))
+    uint32_t md[KB < 10 ? (1 << KB) / 128 : 1];
+    if constexpr (KB < 10) {
+#pragma unroll
+      for (int m = 0; m < (1 << KB) / 128; ++m) md[m] = mask[(lane >> 4) + 4 * m];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
     lds_barrier();
     if (idle) continue;
     if constexpr (KB < 10) {
       constexpr int SB = swap_rbit<LC>();
+      static_assert(regbits_above_lane(), "the output rows' register bits are y bits 7..");
       uint32_t olane = lane;
       asm volatile("" : "+v"(olane));
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         if (((r >> SB) & 1) || !live_above<LC, 10, KB>(r & ~(1 << SB), KB - 1)) continue;
-        const uint32_t y0 = (olane << 1) | reg_pos<LC, 10>(r, SB);
+        const uint32_t R = reg_pos<LC, 10>(r, SB);  // y bits 7.. (regbits_above_lane)
+        const uint32_t y0 = (olane << 1) | R;
         uint32_t ol[2], oh[2];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const int rq = q ? (r | (1 << SB)) : r;
           const uint32_t y = y0 + q;
-          const bool have = int(y) < nv && pr[y];
+          const bool have = (md[R >> 7] >> ((y0 & 31) + q)) & 1;  // int(y) < nv && pr[y]
           Tab T;
           Tabs::load(tabs, y, T);
           uint32_t ml = 0, mh = 0;
           mul_acc(Y.l[rq], Y.h[rq], T, ml, mh);
           uint32_t a = 0, c = 0;
           const uint8_t *row = SH + uint64_t(have ? y : 0u) * sstride + 2 * cbase;
-          if (full) {
+          if (staged) {
+            if (have) {
+              const uint2 d = lds_ld2(lds_addr(regions) + 1024 * (y >> 4) +
+                                      16 * ((4 * (y & 15) + (wave >> 1)) ^ ((y >> 4) & 15)) + 8 * (wave & 1));
+              a = d.x;
+              c = d.y;
+            }
+          } else if (full) {
             const uint2 d = *reinterpret_cast<const uint2 *>(row);
             a = d.x;
             c = d.y;
@@ -436,7 +452,7 @@ reconstruct_n4096(
         if ((pm >> r) & 1) {  // int(y) < nv && pr[y]
           const uint8_t *row = SH + uint64_t(y) * sstride + 2 * cbase;
           uint32_t a = 0, c = 0;
-          if (col0 + COLS <= ncols) {  // staged above
+          if (staged) {
             const uint2 d = lds_ld2(lds_addr(regions) + 1024 * lane + 16 * ((4 * r + (wave >> 1)) ^ (lane & 15)) +
                                     8 * (wave & 1));
             a = d.x;
@@ -478,7 +494,7 @@ reconstruct_n4096(
 }
 
 size_t n4096_scratch_bytes(const CodeParams &p, size_t batch) {
-  return gather_order_bytes(p, batch) + (p.k == 1024 ? batch * kOutImageBytes : 0);
+  return gather_order_bytes(p, batch) + batch * kOutImageBytes;
 }
 
 bool n4096_applicable(const CodeParams &p) {  // the (n, k) instantiated below
@@ -504,8 +520,7 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
       e != hipSuccess)
     return e;
   uint8_t *oimg = static_cast<uint8_t *>(scratch) + gather_order_bytes(p, batch);
-  if (p.k == 1024)
-    hipLaunchKernelGGL(n4096_out_image, dim3(unsigned(batch)), dim3(256), 0, s, d_err_log, d_present, d_pattern,
+  hipLaunchKernelGGL(n4096_out_image, dim3(unsigned(batch)), dim3(256), 0, s, d_err_log, d_present, d_pattern,
                        int(p.n), int(p.nv), t.mtab_tout, oimg);  // tower in, symbols out
   const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
