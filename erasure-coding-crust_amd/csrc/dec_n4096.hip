@@ -150,7 +150,8 @@ reconstruct_n4096(
   const uint64_t ncols = slen / 2;
   const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);
   const uint64_t total = uint64_t(tiles_pp) * batch;
-  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+  const TileSpan span = xcd_span(total);
+  for (uint64_t tile = span.first; tile < span.end; tile += span.step) {
     uint32_t tid = tid0;
     asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63;

@@ -93,6 +93,22 @@ struct TileWalk {
   __device__ __forceinline__ void advance() { next_of(b, i); }
 };
 
+// XCD-affine split of a persistent grid's tiles (blocks b and b + 8 share an
+// XCD and its L2; the placement is a speed hint only, any placement is
+// correct): tiles [0, total) are cut into 8 contiguous spans, span b % 8 walked
+// grid-stride by that group's blocks, so a payload's tiles, and its per-payload
+// tables, masks and gather lists, stay in one L2.  Grids not a multiple of 8
+// (small batches) walk the whole range.
+struct TileSpan {
+  uint64_t first, step, end;
+};
+__device__ __forceinline__ TileSpan xcd_span(uint64_t total) {
+  const uint32_t g = gridDim.x;
+  if (g % 8 != 0 || total < 8ull * g) return {blockIdx.x, g, total};
+  const uint64_t chunk = (total + 7) / 8, lo = (blockIdx.x % 8) * chunk;
+  return {lo + blockIdx.x / 8, g / 8, lo + chunk < total ? lo + chunk : total};
+}
+
 struct Tab {
   uint32_t t[20];
 };
