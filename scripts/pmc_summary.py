@@ -10,7 +10,13 @@ reconstruct kernel's 64-B-per-lane row reads (/1.043).  WRITE_SIZE is exact for
 the 16-B-per-lane stores.
   encode:       fetch = raw x 2 (payload reads are 16 B per lane)
   reconstruct:  fetch = raw / 1.043 (reconstruct_n1024 and _n4096 alike: both
-                read 64 B of a row per lane).  (Until r02 the kernel re-read the
+                read 64 B of a row per lane in the gather).  Since r04
+                reconstruct_n4096 also reads the received output rows y < k
+                (16 B per lane, LDS-DMA) and the 80 KB per-payload output image
+                per tile; those reads count at half weight and are added back as
+                p16 = B x (c k / nv) x shard_len (the rows, expected count) +
+                B x 80 KB (the image: one L2 miss per payload, its tiles
+                sharing one XCD under xcd_span).  (Until r02 the kernel re-read the
                 present data rows y < k in phase 5, 8 B per lane, and this
                 added them back as p5 = B x (present rows < k) x shard_len at
                 half weight.  Since r02 those rows are staged in LDS; the raw
@@ -29,7 +35,7 @@ N = 1 << (NV - 1).bit_length()
 thr = (NV - 1) // 3 + 1
 K = 1 << (thr.bit_length() - 1)
 SL = ((P + 2 * K - 1) // (2 * K)) * 2
-KERNELS = {"encode_k256": "encode", "reconstruct_n1024": "reconstruct",
+KERNELS = {"encode_k256": "encode", "encode_k256w": "encode", "reconstruct_n1024": "reconstruct",
            "encode_k1024_fused": "encode", "reconstruct_n4096": "reconstruct",
            "encode_gen": "encode", "reconstruct_gen": "reconstruct",
            "encode_g": "encode", "reconstruct_g": "reconstruct", "error_locator_g": "error_locator"}
@@ -54,6 +60,11 @@ def per_launch(path, counter):
 fetch = per_launch(f"{src}/FETCH_SIZE/run_counter_collection.csv", "FETCH_SIZE")
 write = per_launch(f"{src}/WRITE_SIZE/run_counter_collection.csv", "WRITE_SIZE")
 p5 = 0  # phase-5 re-reads: none since r02 (LDS staging)
+# reconstruct_n4096 (n > 1024) 16-B-per-lane reads since r04 (see above); the
+# image term assumes one L2 miss per payload (xcd_span)
+p16 = 0
+if N > 1024:
+    p16 = B * (CNT * K / NV) * SL + B * 81920
 res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, kernel-trace only",
        "workload": {"batch": B, "n_validators": NV, "payload_bytes": P, "present": CNT,
                     "shard_len": SL},
@@ -61,7 +72,7 @@ res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, kern
 for k in sorted(set(fetch) | set(write)):
     f, w = fetch.get(k, 0.0), write.get(k, 0.0)
     if k == "reconstruct":
-        fc = (f - p5 / 2) / 1.043 + p5
+        fc = (f - p5 / 2 - p16 / 2) / 1.043 + p5 + p16
     else:
         fc = 2 * f
     res["kernels"][k] = {"fetch_raw_bytes": round(f), "fetch_bytes": round(fc),
