@@ -51,7 +51,9 @@ def pmc_traffic(kernel, nv, plen, cnt, batch):
     (scripts/pmc_traffic.sh + scripts/pmc_summary.py, newest profiles/rNN),
     when it was measured on this workload shape; scaled linearly in batch."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")),
+    # (profiles/rNN/pmc_traffic.json: the default workload; c4_pmc_traffic.json
+    # and the like: other shapes, picked by the workload check below)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "*pmc_traffic.json")),
                        reverse=True):
         try:
             with open(path) as f:
@@ -66,15 +68,17 @@ def pmc_traffic(kernel, nv, plen, cnt, batch):
 
 
 # waves per SIMD of the dominant kernels (launch shapes in csrc/): the SQ
-# counters' per-wave ACTIVE_INST_ANY fraction times this is the share of SIMD
-# cycles that issued an instruction
+# counters' per-wave ACTIVE_INST_ANY / WAVE_CYCLES summed over a SIMD's waves.
+# A wave counts as active while any of its instructions is issuing, and waves
+# issue to different pipes (VALU, LDS, memory, scalar) in the same cycle, so
+# the sum can exceed 1; the per-wave wait fractions are reported beside it.
 _WAVES_PER_SIMD = {"reconstruct": (("reconstruct_n1024<false>", "reconstruct_n1024"), 2),
-                   "encode": (("encode_k256<1024, 0>", "encode_k256<1024>"), 4)}
+                   "encode": (("encode_k256w", "encode_k256<1024, 0>", "encode_k256<1024>"), 4)}
 
 
 def sq_issue(kernel, nv):
-    """SIMD issue fraction of `kernel` from the committed SQ counter summary
-    (scripts/pmc_sq.sh + scripts/sq_summary.py, newest profiles/rNN), measured
+    """SQ issue counters of `kernel` from the committed SQ counter summary
+    (scripts/prof_r4.sh + scripts/sq_summary.py, newest profiles/rNN), measured
     on the default workload shape (nv = 1024): the kernels are bounded by
     instruction issue, not HBM."""
     import glob
@@ -87,8 +91,11 @@ def sq_issue(kernel, nv):
             with open(path) as f:
                 ks = json.load(f)["kernels"]
             k = next(ks[n] for n in names if n in ks)  # (kernel names by round)
-            return {"simd_issue_frac": round(k["frac_active_inst_any"] * waves, 3),
-                    "valu_frac": round(k["frac_active_valu"] * waves, 3),
+            return {"waves_per_simd": waves,
+                    "active_inst_any_per_simd": round(k["frac_active_inst_any"] * waves, 3),
+                    "active_valu_per_simd": round(k["frac_active_valu"] * waves, 3),
+                    "wave_wait_any_frac": round(k["frac_wait_any"], 3),
+                    "wave_wait_inst_any_frac": round(k["frac_wait_inst_any"], 3),
                     "measured_in_this_run": False,
                     "source": os.path.relpath(path, ROOT) + " (stored SQ counter profile)"}
         except (OSError, KeyError, ValueError, StopIteration):
