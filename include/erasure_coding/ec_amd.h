@@ -6,7 +6,8 @@
  * is a hipStream_t (NULL = the legacy default stream).  Calls are asynchronous
  * on `stream` and the caller owns every buffer it passes.  Shapes that need
  * device scratch (k = 1024 encodes, the fast reconstructs' per-payload gather
- * order (4 n bytes per payload), n > 4096 generic kernels,
+ * order (4 n bytes per payload; n = 2048 / 4096 add an 80 KB output-table
+ * image per payload), n > 4096 generic kernels,
  * ECCR_AMD_error_locator / ECCR_AMD_dedup_patterns with batch > 1) use, in the
  * plain calls, a scratch buffer private to (device, stream): the first call of
  * a larger shape on a stream allocates it (hipMalloc, after synchronising that

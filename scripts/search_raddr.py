@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Search a GF(2)-linear 8-B-cell swizzle of the 1024 positions of a wave's
-LDS region (reconstruct_n1024w) under which every exchange
+LDS region (the two-workgroup reconstruct_n1024w of round 4, since removed:
+profiles/r04/NOTES.md) under which every exchange
 access is bank-conflict free (MI355X_MICROARCH.md, LDS): ds_read_b64 in two
 32-lane groups (256 B: cell mod 32 distinct), ds_write_b64 in four 16-lane
 groups (128 B: cell mod 16 distinct).  Layouts (lane bits -> position bits):

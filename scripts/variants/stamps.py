@@ -86,6 +86,8 @@ elif kind == "encw":
     s = rep(s, "  }\n}\n\nhipError_t launch_encode_k256w", "  }\n" + FLUSH + "}\n\nhipError_t launch_encode_k256w")
     names = ["load", "barrier", "stores", "compute"]
 elif kind == "decw":
+    # the two-workgroup reconstruct_n1024w: in dec_n1024.hip as of commit
+    # 0ececd2 only (removed in 9c0fece); check that version out to rerun it
     s = open(f"{ROOT}/erasure-coding-crust_amd/csrc/dec_n1024.hip").read()
     s = rep(s, "namespace ecamd {\nnamespace {", "namespace ecamd {\n__device__ unsigned long long g_stamp[16];\nnamespace {")
     i = s.index("reconstruct_n1024w(")
