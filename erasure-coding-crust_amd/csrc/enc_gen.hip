@@ -188,11 +188,17 @@ __global__ void __launch_bounds__(THREADS)
   const uint32_t tid0 = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid0 >> 6);
   uint8_t *my = regions + wave * REG_BYTES;
 
-  int img = 0;  // table image in LDS: skews 1024 img .. + 1022
-  const auto load_image = [&](int q) {
-    lds_barrier();  // every wave is done with the current tables
-    Tabs::copy_image<THREADS>(tabs, t.timg_t + q * kTabImageBytes, tid0);
-    lds_barrier();
+  int img = 0;  // table image in LDS (or requested): skews 1024 img .. + 1022
+  // n = 2048 / 4096: the next coset's (or the next tile's index-0) image is
+  // requested by LDS-DMA as soon as every wave is past the current coset's
+  // FFT, so it lands behind that coset's row stores; `pending` until retired
+  bool pending = false;
+  const auto retire = [&]() __attribute__((always_inline)) {
+    if (pending) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
+      pending = false;
+    }
   };
   // tower images: the transforms run in tower coordinates
   Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);  // skews 0..1022: every coset of n <= 1024
@@ -259,10 +265,7 @@ __global__ void __launch_bounds__(THREADS)
     }
 
     // ---- IFFT_k (index 0): pass A, exchange, pass B -> layout B
-    if (img != 0) {  // the previous tile ended on a higher image
-      load_image(0);
-      img = 0;
-    }
+    retire();  // the index-0 image requested by the previous tile's last coset
     const uint32_t lbA = tlin((16 * lane) & (Gm::K - 1));
     constexpr int S0 = tower_sub_min(0);
     ipassg<0, (M < 4 ? M : 4), M, S0>(s, tabs, lbA);
@@ -301,10 +304,7 @@ __global__ void __launch_bounds__(THREADS)
       fpassg<0, (M < 4 ? M : 4), M, SMc>(s, tabs, tlin((16 * lane) & (Gm::K - 1)) ^ lo);
     };
     for (int sh = int(Gm::K); sh < n && sh < nv; sh += int(Gm::K)) {
-      if ((sh >> 10) != img) {  // (load_image waits for every wave's last table reads)
-        img = sh >> 10;
-        load_image(img);
-      }
+      retire();  // this coset's image
       s = coef;
 #pragma unroll
       for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(s.l[r]), "+v"(s.h[r]));
@@ -318,10 +318,20 @@ __global__ void __launch_bounds__(THREADS)
         for (int r = 0; r < 16; ++r) s.l[r] = tower_lo(s.l[r], s.h[r], tk);
       }
       stage<M>(s, my, lane);  // own region: no other wave touches it since the barrier above
-      lds_barrier();
+      lds_barrier();  // (every wave is past this coset's FFT: its tables are free)
+      {
+        const int nsh = sh + int(Gm::K);
+        const int next = nsh < n && nsh < nv ? nsh >> 10 : 0;
+        if (next != img) {
+          Tabs::dma_image<THREADS>(tabs, t.timg_t + next * kTabImageBytes, tid);
+          img = next;
+          pending = true;
+        }
+      }
       store_rows<M>(regions, SH, sstride, uint32_t(sh), nv, piece0, npieces, tid);
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
 }
 
 template <int M>
