@@ -155,8 +155,8 @@ elif kind == "dec4":
             "        Tabs::dma_image<THREADS>(tabs, t.timg_t + qnext * kTabImageBytes, tq);\n        __builtin_amdgcn_sched_barrier(0);\n      }\n      STAMP(3);\n")
     s = rep(s, "        asm volatile(\"\" : \"+v\"(P.l[r]), \"+v\"(P.h[r]), \"+v\"(Qa.l[r]), \"+v\"(Qa.h[r]));\n      __builtin_amdgcn_sched_barrier(0);\n    };",
             "        asm volatile(\"\" : \"+v\"(P.l[r]), \"+v\"(P.h[r]), \"+v\"(Qa.l[r]), \"+v\"(Qa.h[r]));\n      __builtin_amdgcn_sched_barrier(0);\n      STAMP(4);\n    };")
-    s = rep(s, "    const uint64_t cbase = col0 + 4 * wave;\n    lds_barrier();  // every wave is done with the FFT tables\n",
-            "    const uint64_t cbase = col0 + 4 * wave;\n    STAMP(5);\n    lds_barrier();  // every wave is done with the FFT tables\n")
+    s = rep(s, "    lds_barrier();  // every wave is done with the FFT tables\n",
+            "    STAMP(5);\n    lds_barrier();  // every wave is done with the FFT tables\n")
     s = rep(s, "    lds_barrier();\n    if (idle) continue;\n", "    lds_barrier();\n    STAMP(6);\n    if (idle) continue;\n")
     s = rep(s, "        reinterpret_cast<uint4 *>(dst)[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);\n      }\n    }\n  }\n}",
             "        reinterpret_cast<uint4 *>(dst)[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);\n      }\n    }\n    STAMP(7);\n  }\n" + FLUSH + "}")
