@@ -83,4 +83,6 @@ def payloads_torch(seeds, length: int, device="cuda"):
     z = (z ^ lsr(z, 30)) * (0xBF58476D1CE4E5B9 - (1 << 64))
     z = (z ^ lsr(z, 27)) * (0x94D049BB133111EB - (1 << 64))
     z = z ^ lsr(z, 31)
-    return z.view(torch.uint8).view(len(seeds), words * 8)[:, :length]
+    out = z.view(torch.uint8).view(len(seeds), words * 8)
+    # rows of exactly `length` bytes (pstride = length), not a strided view
+    return out if length == words * 8 else out[:, :length].contiguous()

@@ -452,6 +452,43 @@ def test_batch_past_4GiB(oracle, nv):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("nv,plen,batch", [(3069, 1_000_000, 67), (4096, 300_001, 411)])
+def test_batch_xcd_spans(oracle, nv, plen, batch):
+    """reconstruct_n4096's XCD-affine tile spans (ec_device.hpp xcd_span): with
+    at least 8 x grid tiles the tiles are cut into 8 contiguous spans; these
+    shapes give spans of unequal length (2,077 tiles at k = 512, 2,055 at
+    k = 1024) and spans that start and end inside a payload.  Every payload
+    round-trips (a skipped tile would leave the 0xAA prefill); the first, the
+    last and one mid-batch payload are compared with the oracle."""
+    import torch
+    n, k, thr = E.code_params(nv)
+    sl = E.shard_len(nv, plen)
+    ss = (sl + 63) // 64 * 64
+    tiles = (sl // 2 + 31) // 32 * batch
+    assert tiles >= 8 * 256 and tiles % 8 != 0  # the span path on a 256-CU part, unequal spans
+    seeds = list(range(91_000, 91_000 + batch))
+    d_pay = synth.payloads_torch(seeds, plen)
+    pres = synth.present_masks([10**6 + s for s in seeds], nv, thr, n)
+    d_pr = torch.from_numpy(pres).cuda()
+    d_sh = _prefilled((batch, nv, ss))
+    d_el = torch.zeros((batch, n), dtype=torch.int16, device="cuda")
+    d_out = _prefilled((batch, sl * k))
+    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+    E.error_locator(nv, d_pr, batch, d_el)
+    E.reconstruct_batch(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k)
+    torch.cuda.synchronize()
+    assert torch.equal(d_out[:, :plen], d_pay)
+    assert not d_out[:, plen:].any()
+    for b in (0, batch // 2, batch - 1):
+        p = synth.payload(seeds[b], plen).tobytes()
+        ref = oracle.encode(nv, p)
+        assert b"".join(ref) == d_sh[b, :, :sl].cpu().numpy().tobytes(), b
+        keep = [ref[i] if pres[b][i] else None for i in range(nv)]
+        assert d_out[b].cpu().numpy().tobytes() == oracle.reconstruct(nv, keep), b
+    del d_pay, d_sh, d_out
+    torch.cuda.empty_cache()
+
+
 # ------------------------------------------- erasure patterns per reconstruct kernel
 def _pattern_rows(nv, n, k, thr, rng):
     """One present mask per pattern the reference's gap / erased-index handling
@@ -1104,3 +1141,4 @@ def test_locator_rows_every_pattern(oracle):
             erased = (pres[b][:n] == 0).astype(np.uint8)
             ep = oracle.error_poly(erased, n)[:n].astype(np.int64) % 65535
             assert ((el[b].astype(np.int64) % 65535) == ep).all(), (nv, b)
+
