@@ -257,9 +257,11 @@ reconstruct_n4096(
           Qq.l[r] = x.x;
           Qq.h[r] = x.y;
         }
-        // the two waves of a SIMD (w, w + 4) alternate the higher issue
-        // priority from quarter to quarter (as reconstruct_n1024's passes)
-        if (((wave >> 2) ^ uint32_t(q)) & 1) __builtin_amdgcn_s_setprio(2);
+        // n = 2048: the two waves of a SIMD (w, w + 4) alternate the higher
+        // issue priority from half to half (as reconstruct_n1024's passes);
+        // n = 4096: equal priority (alternating: config 4 reconstruct 7.81
+        // against 7.65 ms; n = 2048 without: 2.92-2.98 against 2.88-2.89)
+        if (NQ == 2 && (((wave >> 2) ^ uint32_t(q)) & 1)) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(0);
         // -> layout C; quarter 0 is at index 0
         ifft1024<q == 0, tower_sub_min(q)>(Qq, tabs, my, lq);
