@@ -222,7 +222,7 @@ __device__ __forceinline__ uint2 load8_any(const uint8_t *p, uint32_t avail) {
 }
 
 // The two waves of a SIMD (w, w + 4) take turns at the higher issue priority
-// (pass A: w + 4, pass B: w, pass C to the FFT: w + 4, output: w, gather:
+// (pass A: w + 4, pass B: w, pass C to the FFT: w + 4, output and gather:
 // equal), so
 // neither runs far ahead and then idles at the tile barrier while the other
 // finishes alone (the arbiter otherwise favours the older wave throughout).
@@ -749,7 +749,9 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024(
       fb(0, 1, T[0]);  // stage 0
       fb(2, 3, T[1]);
     }
-    prio_lead(!(wave_s & 4));  // the output: w leads (11.26 -> 11.19 ms at B = 4096)
+    // the output at equal priority (round 4: 11.00-11.03 against 11.05 ms with
+    // w leading, which round 3 measured as the better one, 11.26 -> 11.19)
+    __builtin_amdgcn_s_setprio(0);
 
     // ---- phase 5: y = 4*lane + q; columns col0 + 4*wave + c (decode_main:185-188,
     // reconstructSub:138-149).  No workgroup barrier: the operands were
