@@ -188,6 +188,23 @@ def cpu_size_rate(nv, plen, cnt, seconds, threads):
             f"GiBps_{threads}threads": round(dn * plen / wn / 2**30, 6)}
 
 
+def device_info(local):
+    """This rank's device: index, name and PCI location (a multi-GPU line must
+    show N distinct bus ids).  Works without a GPU (CPU tests): nulls."""
+    info = {"device": local, "name": None, "pci_bus_id": None}
+    try:
+        if torch.cuda.is_available():
+            p = torch.cuda.get_device_properties(local)
+            info["name"] = p.name
+            bus = getattr(p, "pci_bus_id", None)
+            if bus is not None:
+                info["pci_bus_id"] = "%04x:%02x:%02x" % (getattr(p, "pci_domain_id", 0), bus,
+                                                        getattr(p, "pci_device_id", 0))
+    except Exception as exc:  # noqa: BLE001 (reported, never fatal)
+        info["error"] = f"{type(exc).__name__}: {exc}"[:120]
+    return info
+
+
 def device_bandwidth(dev, nbytes=1 << 30, reps=5):
     """Measured device bandwidth on this box (the roofline also
     against a measured copy): a 1 GiB device-to-device copy (read + write
@@ -414,6 +431,22 @@ def launch_ranks(n, backend, grace_s=60.0):
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
     procs = []
+
+    def forward(signo, _frame):  # the parent killed alone must not leave ranks holding GPUs
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        deadline = time.monotonic() + 15
+        for p in procs:
+            try:
+                p.wait(max(deadline - time.monotonic(), 0.1))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        os._exit(128 + signo)
+
+    for signo in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(signo, forward)
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -584,6 +617,8 @@ def main():
     if dist:
         dist.barrier()
     elapsed = sharding.max_over_ranks(t1 - t0, dist, dev if backend == "nccl" else None)
+    ranks_detail = sharding.rank_table(dict(device_info(local), rank=rank,
+                                            step_ms=round((t1 - t0) / args.steps * 1e3, 3)), dist)
 
     # sanity: the last step's reconstruction equals the payloads (round trip)
     ok = bool(torch.equal(d_out[:, :plen], d_pay))
@@ -608,6 +643,10 @@ def main():
         # ranks share GPUs only in the gloo rehearsal mode (ECCR_BENCH_BACKEND)
         "n_gpus": world if backend == "nccl" else min(world, max(torch.cuda.device_count(), 1)),
         "ranks": world,
+        "world_size": dist.get_world_size() if dist else 1,
+        # per rank: its device and PCI bus id and its own step time (the value
+        # uses the slowest, ms_per_step); distinct bus ids = distinct GPUs
+        "ranks_detail": ranks_detail,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u16",

@@ -1,8 +1,8 @@
 // cimg.hpp — multiply tables from the element-indexed compact image
 // (ec_kernels.hpp kCImg*, DevTables::cimg) resident at LDS address 0: the
-// n = 1024 encode (enc_k256w.hip) and reconstruct (dec_n1024.hip, the
-// two-workgroup form).  Kernels using it declare no static LDS
-// (prepare_kernel checks), so the image starts at absolute LDS address 0.
+// n = 1024 encode (enc_k256w.hip), its only user.  Kernels using it declare
+// no static LDS (prepare_kernel checks), so the image starts at absolute LDS
+// address 0.
 #pragma once
 
 #include "ec_device.hpp"

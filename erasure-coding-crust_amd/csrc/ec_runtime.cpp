@@ -35,21 +35,18 @@ struct DeviceState {
   unsigned long loc_hits = 0, loc_misses = 0;
   std::mutex ss_mu;
   std::list<std::shared_ptr<StreamScratchEntry>> ss;  // per-stream scratch, most recent first
+  std::list<std::shared_ptr<StreamScratchEntry>> ss_dead;  // evicted, freed by drain_dead()
 };
 
 // One stream's scratch buffer.  `mu` is held by a StreamScratch lease while
-// its caller enqueues; the buffer is freed by the last owner (the device list
-// or a lease), after the device has drained (see ec_runtime.hpp).
+// its caller enqueues.  An evicted entry is never freed by a lease's
+// destructor (that could be inside another thread's graph capture, ADVICE
+// r04): it waits in DeviceState::ss_dead for drain_dead() (see ec_runtime.hpp).
 struct StreamScratchEntry {
   hipStream_t s = nullptr;
   void *p = nullptr;
   size_t cap = 0;
   std::mutex mu;
-  ~StreamScratchEntry() {
-    if (!p) return;
-    (void)hipDeviceSynchronize();
-    (void)hipFree(p);
-  }
 };
 
 namespace {
@@ -343,15 +340,41 @@ std::shared_ptr<const Locator> cached_locator(DeviceState *d, const CodeParams &
   return L;
 }
 
+namespace {
+// Frees the evicted entries nobody holds any more, after a device
+// synchronisation (their streams may be gone, so the whole device is waited
+// for).  Called where waiting is allowed: never while `s` is being captured.
+void drain_dead(DeviceState *d, hipStream_t s) {
+  std::list<std::shared_ptr<StreamScratchEntry>> dead;
+  {
+    std::lock_guard<std::mutex> lk(d->ss_mu);
+    if (d->ss_dead.empty()) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+    for (auto it = d->ss_dead.begin(); it != d->ss_dead.end();)
+      if (it->use_count() == 1) {  // no lease holds it
+        dead.push_back(std::move(*it));
+        it = d->ss_dead.erase(it);
+      } else {
+        ++it;
+      }
+  }
+  if (dead.empty()) return;
+  (void)hipDeviceSynchronize();
+  for (auto &e : dead)
+    if (e->p) (void)hipFree(e->p);
+}
+}  // namespace
+
 StreamScratch::StreamScratch(DeviceState *d, hipStream_t s, size_t bytes) : want_(bytes) {
   if (!d || bytes == 0) return;
+  drain_dead(d, s);
   const size_t limit = g_scratch_limit;
   if (limit && bytes > limit) {  // as if hipMalloc had failed
     set_error("erasure_coding_crust(amd): scratch of " + std::to_string(bytes) +
               " bytes exceeds the limit set by ECCR_AMD_set_scratch_limit");
     return;
   }
-  std::shared_ptr<StreamScratchEntry> evicted;  // dropped after ss_mu is released
   {
     std::lock_guard<std::mutex> lk(d->ss_mu);
     auto it = d->ss.begin();
@@ -360,7 +383,7 @@ StreamScratch::StreamScratch(DeviceState *d, hipStream_t s, size_t bytes) : want
       d->ss.splice(d->ss.begin(), d->ss, it);  // most recent first
     } else {
       if (d->ss.size() >= kStreamScratch) {
-        evicted = std::move(d->ss.back());
+        d->ss_dead.push_back(std::move(d->ss.back()));  // freed by a later drain_dead()
         d->ss.pop_back();
       }
       auto e = std::make_shared<StreamScratchEntry>();
@@ -369,7 +392,6 @@ StreamScratch::StreamScratch(DeviceState *d, hipStream_t s, size_t bytes) : want
     }
     e_ = d->ss.front();
   }
-  evicted.reset();  // the last owner frees it (after a device synchronisation)
   e_->mu.lock();
   locked_ = true;
   if (e_->cap < bytes) {
@@ -403,13 +425,20 @@ bool release_stream_scratch(DeviceState *d, hipStream_t s) {
       }
   }
   if (!e) return false;
-  std::lock_guard<std::mutex> lk(e->mu);  // no caller is enqueueing on it
-  if (e.use_count() == 1 && e->p) {       // nobody else can reach it any more
-    (void)hipStreamSynchronize(s);
-    (void)hipFree(e->p);
-    e->p = nullptr;
-    e->cap = 0;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);  // no caller is enqueueing on it
+    if (e.use_count() == 1 && e->p) {       // nobody else can reach it any more
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(e->p);
+      e->p = nullptr;
+      e->cap = 0;
+    }
   }
+  if (e->p) {  // a lease still holds it: freed by a later drain
+    std::lock_guard<std::mutex> lk(d->ss_mu);
+    d->ss_dead.push_back(std::move(e));
+  }
+  drain_dead(d, s);
   return true;
 }
 

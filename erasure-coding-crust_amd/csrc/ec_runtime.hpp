@@ -59,10 +59,14 @@ class ScratchLease {
 // call allocates, records and waits on nothing, so it can be captured into a
 // hipGraph, and calls on different streams never wait on each other.  At most
 // kStreamScratch streams per device keep a buffer; beyond that the least
-// recently used entry is dropped, and its buffer is freed by its last holder
-// after a hipDeviceSynchronize (the stream handle may be dangling, so the
-// whole device is waited for: rare, but it does wait on every stream).
-// ECCR_AMD_release_stream_scratch releases one stream's buffer explicitly.
+// recently used entry is evicted to a deferred list.  A lease's destructor
+// never frees or synchronises (it may run inside a graph capture); evicted
+// buffers nobody holds are freed after a hipDeviceSynchronize at the start of
+// a later lease on a stream that is not being captured, or by
+// ECCR_AMD_release_stream_scratch (the stream handle of an evicted entry may
+// be dangling, so the whole device is waited for: rare, but it does wait on
+// every stream).  ECCR_AMD_release_stream_scratch releases one stream's
+// buffer explicitly.
 // ok() false (error set) if the allocation failed or exceeds the scratch limit.
 constexpr size_t kStreamScratch = 64;
 struct StreamScratchEntry;

@@ -58,6 +58,18 @@ def max_over_ranks(value: float, dist=None, device=None) -> float:
     return float(t.item())
 
 
+def rank_table(info: dict, dist=None) -> list[dict]:
+    """Every rank's `info` (its device, PCI bus id, own step time ...), in rank
+    order, on every rank: the evidence that a multi-GPU line ran on N distinct
+    devices and how far the slowest rank is from the others (VERDICT r04
+    item 7).  One process: [info]."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [dict(info)]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, dict(info))
+    return out
+
+
 def scatter_from_root(dist, src, dst, rank: int, world: int, root: int = 0) -> None:
     """Root sends slice r of `src` ([world][...]; only read on the root) to rank
     r; every rank (root included) receives its slice into `dst`.  One grouped

@@ -236,3 +236,28 @@ class RefEC(_Lib):
         if e:
             raise CodecError(e)
         return done.value, wall.value, te.value, td.value
+
+
+class Checker:
+    """What the tests compare byte outputs with: the
+    reference ec-cpp itself (RefEC) for encode / reconstruct /
+    reconstruct_from_systematic when oracle/_ref/libecref.so was built, the C
+    restatement otherwise; every internal the reference does not export
+    (error_poly, afft, walsh, tables, ...) from the restatement.  `kind` says
+    which one checked the bytes: "reference" or "restatement"."""
+
+    BYTE_OUTPUTS = ("encode", "reconstruct", "reconstruct_from_systematic", "params", "threshold",
+                    "shard_len")
+
+    def __init__(self, restatement: "Oracle", ref: "RefEC | None" = None):
+        self.restatement = restatement
+        self.ref = ref
+        self.kind = "reference" if ref is not None else "restatement"
+
+    @classmethod
+    def default(cls) -> "Checker":
+        return cls(Oracle(), RefEC() if RefEC.available() else None)
+
+    def __getattr__(self, name):
+        src = self.ref if (self.ref is not None and name in self.BYTE_OUTPUTS) else self.restatement
+        return getattr(src, name)

@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Diagnostic (wrong-result) variants of encode_k256w for the time account of
+the headline encode.  Each removes one kind of work and
+keeps every instruction of the rest, so the kernel-time difference is what
+that work costs in the real interleaving:
+
+  enc_diag.py KIND OUTDIR   writes OUTDIR/enc_k256w.hip and OUTDIR/cimg.hpp
+    nobar   the per-tile workgroup barriers dropped (LDS races: garbage rows)
+    nost    the row stores dropped (LDS reads kept; nothing written)
+    nold    payload loads replaced by lane-derived words
+    nostg   row stores dropped, their LDS reads and addresses kept (asm-consumed)
+    stplain row stores without the nontemporal hint
+    noprio  no s_setprio around the store phases
+    notab   multiply tables from VALU-derived words instead of LDS reads
+    cmp     nobar + nost + nold: the transforms alone
+    cmpt    cmp + notab: the register-only instruction stream
+    clk     wave 0 of every workgroup sums s_memtime (shader clock) and
+            s_memrealtime (100 MHz) over its lifetime: the clock under load
+            (scripts/variants/clk_run.py); combine as e.g. clk+nostg
+
+Build: scripts/build_var.sh diag_KIND "" enc_k256w.hip=OUT/enc_k256w.hip cimg.hpp=OUT/cimg.hpp"""
+import os
+import sys
+
+ROOT = __file__.rsplit("/scripts/", 1)[0]
+CS = f"{ROOT}/erasure-coding-crust_amd/csrc"
+kind, out = sys.argv[1], sys.argv[2]
+os.makedirs(out, exist_ok=True)
+enc = open(f"{CS}/enc_k256w.hip").read()
+cim = open(f"{CS}/cimg.hpp").read()
+
+
+READER = '''
+extern "C" int ECCR_DIAG_stamps(unsigned long long *out, int n, int reset) {
+  if (n > 16) n = 16;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ecamd::g_stamp), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    z[2] = z[4] = ~0ull;  // atomicMin slots
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ecamd::g_stamp), z, sizeof(z));
+  }
+  return n;
+}
+'''
+
+
+def rep(s, old, new):
+    assert s.count(old) == 1, old[:70]
+    return s.replace(old, new)
+
+
+ALIAS = {"cmp": ["nobar", "nost", "nold"], "cmpt": ["nobar", "nost", "nold", "notab"]}
+kinds = [x for part in kind.split("+") for x in ALIAS.get(part, [part])]
+for k in kinds:
+    if k == "nobar":
+        enc = rep(enc, "const auto rsync = [&]() __attribute__((always_inline)) { lds_barrier(); };",
+                  "const auto rsync = [&]() __attribute__((always_inline)) { asm volatile(\"\" ::: \"memory\"); };")
+    elif k == "nost":
+        enc = rep(enc, "  asm volatile(\"\" : \"+v\"(lane));  // recomputed here, not kept live across the FFTs\n",
+                  "  asm volatile(\"\" : \"+v\"(lane));\n  if (s0 != 0xFFFFFFFFu) {\n    then();\n    return;\n  }\n")
+    elif k == "nostg":
+        enc = rep(enc, "      __builtin_nontemporal_store(val, reinterpret_cast<v4u *>(dst + it * dstep));  // written once\n",
+                  "      asm volatile(\"\" :: \"v\"(val), \"v\"(dst + it * dstep));\n")
+    elif k == "stplain":
+        enc = rep(enc, "      __builtin_nontemporal_store(val, reinterpret_cast<v4u *>(dst + it * dstep));  // written once\n",
+                  "      *reinterpret_cast<v4u *>(dst + it * dstep) = val;\n")
+    elif k == "noprio":
+        enc = enc.replace("__builtin_amdgcn_s_setprio(1);", "").replace("__builtin_amdgcn_s_setprio(0);", "")
+    elif k == "clk":
+        enc = rep(enc, "namespace ecamd {\nnamespace {", "namespace ecamd {\n__device__ unsigned long long g_stamp[16];\nnamespace {")
+        enc = rep(enc, "  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];\n",
+                  "  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];\n"
+                  "  const uint64_t clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();\n")
+        enc = rep(enc, "  }\n}\n\nhipError_t launch_encode_k256w",
+                  "  }\n  if (threadIdx.x == 0) {\n"
+                  "    atomicAdd(&g_stamp[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - clk_t0));\n"
+                  "    atomicAdd(&g_stamp[1], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - clk_r0));\n"
+                  "    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();\n"
+                  "    atomicMin(&g_stamp[2], (unsigned long long)clk_r0);\n"
+                  "    atomicMax(&g_stamp[3], (unsigned long long)clk_r0);\n"
+                  "    atomicMin(&g_stamp[4], r1);\n"
+                  "    atomicMax(&g_stamp[5], r1);\n"
+                  "    atomicAdd(&g_stamp[6], 1ull);\n  }\n"
+                  "}\n\nhipError_t launch_encode_k256w")
+        enc += READER
+    elif k == "nold":
+        enc = rep(enc, "      for (int u = 0; u < 4; ++u) d[u] = *reinterpret_cast<const v4u *>(src + u * 2 * K);\n",
+                  "      for (int u = 0; u < 4; ++u) d[u] = v4u{uint32_t(pw) * 0x9E3779B1u + u, uint32_t(fb) ^ 0x5bd1e995u, q * 77u, inst};\n")
+    elif k == "notab":
+        for typ, n in (("SubTab", 5), ("F9Tab", 16), ("Tab", 20)):
+            start = cim.index(f"__device__ __forceinline__ void ctab(uint32_t lt, uint32_t u, {typ} &T) {{")
+            end = cim.index("\n}\n", start) + 3
+            body = (f"__device__ __forceinline__ void ctab(uint32_t lt, uint32_t u, {typ} &T) {{\n"
+                    f"  const uint32_t a = lt ^ u;\n"
+                    f"#pragma unroll\n  for (int i = 0; i < {n}; ++i) T.t[i] = (a + uint32_t(i) * 0x01010101u) & 0x3F3F3F3Fu;\n}}\n")
+            cim = cim[:start] + body + cim[end:]
+    else:
+        raise SystemExit(f"unknown kind {k}")
+open(f"{out}/enc_k256w.hip", "w").write(enc)
+open(f"{out}/cimg.hpp", "w").write(cim)
+print("wrote", out, kinds)

@@ -69,7 +69,7 @@ elif kind == "dec":
     s = rep(s, "    if constexpr (!PACKED) __syncthreads();  // packed",
             "    STAMP(0);\n    if constexpr (!PACKED) __syncthreads();\n    STAMP(1);  // packed")
     s = rep(s, "    prio_lead(wave_s & 4);\n    // ---- phases 3 + 4a", "    prio_lead(wave_s & 4);\n    STAMP(2);\n    // ---- phases 3 + 4a")
-    s = rep(s, "    prio_lead(!(wave_s & 4));  // the output", "    STAMP(3);\n    prio_lead(!(wave_s & 4));  // the output")
+    s = rep(s, "    // the output at equal priority", "    STAMP(3);\n    // the output at equal priority")
     s = rep(s, "    __builtin_amdgcn_s_setprio(0);  // the next tile's gather: equal\n  }\n",
             "    __builtin_amdgcn_s_setprio(0);  // the next tile's gather: equal\n    STAMP(4);\n  }\n" + FLUSH)
     names = ["gather", "barriers", "ifft", "deriv+fft", "output"]
@@ -79,8 +79,9 @@ elif kind == "encw":
     s = rep(s, "  __syncthreads();\n\n  const uint64_t npieces", "  __syncthreads();\n" + STAMP + "\n  const uint64_t npieces")
     s = rep(s, "    const auto rsync = [&]() __attribute__((always_inline)) { lds_barrier(); };",
             "    const auto rsync = [&]() __attribute__((always_inline)) { STAMP(3); lds_barrier(); STAMP(1); };")
-    s = rep(s, "      __builtin_amdgcn_s_setprio(1);\n", "      STAMP(3);\n      __builtin_amdgcn_s_setprio(1);\n")
-    s = rep(s, "      __builtin_amdgcn_s_setprio(0);\n    };", "      __builtin_amdgcn_s_setprio(0);\n      STAMP(2);\n    };")
+    # both store lambdas (store, store_last)
+    s = rep(s, "      __builtin_amdgcn_s_setprio(1);\n", "      STAMP(3);\n      __builtin_amdgcn_s_setprio(1);\n", 2)
+    s = rep(s, "      __builtin_amdgcn_s_setprio(0);\n    };", "      __builtin_amdgcn_s_setprio(0);\n      STAMP(2);\n    };", 2)
     s = rep(s, "    // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)\n",
             "    STAMP(0);\n    // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)\n")
     s = rep(s, "  }\n}\n\nhipError_t launch_encode_k256w", "  }\n" + FLUSH + "}\n\nhipError_t launch_encode_k256w")
@@ -109,39 +110,34 @@ elif kind == "enc4":
             "  Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);  // index 0 (the IFFT)\n  __syncthreads();\n" + STAMP)
     s = rep(s, "    // systematic shards 0..1023 = the data symbols (poly_encoder.hpp:239)\n",
             "    STAMP(0);\n    // systematic shards 0..1023 = the data symbols (poly_encoder.hpp:239)\n")
-    s = rep(s, "    // the index-0 tables (the last tile's DMA) landed; the regions are free\n",
-            "    STAMP(1);\n    // the index-0 tables (the last tile's DMA) landed; the regions are free\n")
-    s = rep(s, "    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    lds_barrier();\n    if (!idle) {\n      to_tower(g0, g1);",
-            "    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    lds_barrier();\n    STAMP(2);\n    if (!idle) {\n      to_tower(g0, g1);")
+    s = rep(s, "    // the index-0 tables (the last tile's DMA, issued before the 16 fast-form\n",
+            "    STAMP(1);\n    // the index-0 tables (the last tile's DMA, issued before the 16 fast-form\n")
+    s = rep(s, "    lds_barrier();\n    if (!idle) {\n      to_tower(g0, g1);",
+            "    lds_barrier();\n    STAMP(2);\n    if (!idle) {\n      to_tower(g0, g1);")
     s = rep(s, "    lds_barrier();  // every wave is done with the index-0 tables\n",
             "    STAMP(3);\n    lds_barrier();  // every wave is done with the index-0 tables\n")
-    s = rep(s, "      asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // coset s's tables and coefficients landed\n      lds_barrier();  // (all waves' slices) and the regions are free\n",
-            "      STAMP(4);\n      asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // coset s's tables and coefficients landed\n      lds_barrier();  // (all waves' slices) and the regions are free\n      STAMP(2);\n")
+    s = rep(s, "      constexpr uint32_t s = decltype(cs)::value;\n",
+            "      constexpr uint32_t s = decltype(cs)::value;\n      STAMP(4);\n")
+    s = rep(s, "      lds_barrier();  // (all waves' slices) and the regions are free\n",
+            "      lds_barrier();  // (all waves' slices) and the regions are free\n      STAMP(2);\n")
     s = rep(s, "        to_tower(g0, g1);  // back to symbol coordinates\n      }\n",
             "        to_tower(g0, g1);  // back to symbol coordinates\n      }\n      STAMP(5);\n")
-    s = rep(s, """      for (uint32_t hf = 0; hf < 2; ++hf) {
-        if (hf) lds_barrier();
+    s = rep(s, """        if (hf) lds_barrier();
         if (!idle) stage_half(g0, g1, my, lane, wave, hf);
         lds_barrier();
-        if (hf == 0)  // every wave is past its FFT: the next set (index 0 after the last coset)
-          Tabs::dma_image<THREADS>(tabs, t.timg_t + (s + 1 < ncos ? s + 1 : 0) * kTabImageBytes, tid);
-        store_half(regions, SH, sstride, s * K + 512 * hf, nv, piece0, npieces, wave, lane);
-      }""", """      for (uint32_t hf = 0; hf < 2; ++hf) {
-        if (hf) lds_barrier();
+        if (hf == 0)""", """        if (hf) lds_barrier();
         STAMP(7);
         if (!idle) stage_half(g0, g1, my, lane, wave, hf);
         STAMP(8);
         lds_barrier();
         STAMP(7);
-        if (hf == 0)  // every wave is past its FFT: the next set (index 0 after the last coset)
-          Tabs::dma_image<THREADS>(tabs, t.timg_t + (s + 1 < ncos ? s + 1 : 0) * kTabImageBytes, tid);
-        STAMP(9);
-        store_half(regions, SH, sstride, s * K + 512 * hf, nv, piece0, npieces, wave, lane);
-        STAMP(10);
-      }""")
+        if (hf == 0)""")
+    s = rep(s, "        store_half(regions, SH, sstride, s * K + 512 * hf, nv, piece0, npieces, wave, lane);\n      }\n    };",
+            "        STAMP(9);\n        store_half(regions, SH, sstride, s * K + 512 * hf, nv, piece0, npieces, wave, lane);\n        STAMP(10);\n      }\n    };")
     s = rep(s, "    if (ncos > 3) coset(std::integral_constant<uint32_t, 3>());\n  }\n",
             "    if (ncos > 3) coset(std::integral_constant<uint32_t, 3>());\n    STAMP(1);\n  }\n" + FLUSH)
-    names = ["load", "sys+stage+stores", "vmcnt0+barrier", "ifft", "coef+barrier", "fft", "-", "barriers", "stage", "dma", "stores"]
+    names = ["load", "sys+stage+stores", "vmcnt+barrier", "ifft", "coef+barrier", "fft", "-", "barriers", "stage",
+             "dma+coef", "stores"]
 elif kind == "dec4":
     s = open(f"{ROOT}/erasure-coding-crust_amd/csrc/dec_n4096.hip").read()
     s = rep(s, "namespace ecamd {\nnamespace {", "namespace ecamd {\n__device__ unsigned long long g_stamp[16];\nnamespace {")

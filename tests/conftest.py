@@ -21,6 +21,18 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def oracle():
+    """The byte-output checker: the reference ec-cpp (oracle/_ref, built from
+    /root/reference by oracle/Makefile; it travels to the GPU box with the
+    tree) when present, else the C restatement; internals from the restatement
+    (oracle.Checker).  test_oracle.py pins the restatement itself."""
+    import oracle as orc
+    orc.build()
+    return orc.Checker.default()
+
+
+@pytest.fixture(scope="session")
+def restatement():
+    """The C restatement alone (oracle/ec_oracle.c), for the tests that pin it."""
     import oracle as orc
     orc.build()
     return orc.Oracle()

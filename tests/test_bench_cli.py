@@ -45,3 +45,35 @@ def test_launched_ranks_failure_propagates():
     assert r.returncode != 0, (r.stdout, r.stderr[-2000:])
     assert r.stderr.count("Traceback") == 2, r.stderr[-3000:]
     assert not any(l.startswith("{") for l in r.stdout.splitlines())
+
+
+def test_parent_signal_terminates_ranks(tmp_path):
+    """killing only the launching parent (SIGTERM to its pid) must
+    not leave its rank processes running (they would keep their GPUs).  The
+    ranks here are stand-ins that record their pid and sleep."""
+    import signal
+    import time
+    sleeper = tmp_path / "rank.py"
+    sleeper.write_text("import os, time\n"
+                       f"open(os.path.join({str(tmp_path)!r}, 'pid%s' % os.environ['RANK']), 'w')"
+                       ".write(str(os.getpid()))\n"
+                       "time.sleep(300)\n")
+    driver = tmp_path / "driver.py"
+    driver.write_text("import sys\n"
+                      f"sys.path.insert(0, {ROOT!r})\n"
+                      "import bench\n"
+                      f"bench.__file__ = {str(sleeper)!r}\n"
+                      "sys.exit(bench.launch_ranks(2, 'gloo'))\n")
+    p = subprocess.Popen([sys.executable, str(driver)], cwd=ROOT)
+    pids = []
+    for _ in range(600):
+        pids = [tmp_path / f"pid{r}" for r in range(2)]
+        if all(f.exists() and f.read_text() for f in pids):
+            break
+        time.sleep(0.1)
+    pids = [int(f.read_text()) for f in pids]
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(60) == 128 + signal.SIGTERM
+    for pid in pids:  # both ranks are gone (reaped by the parent)
+        with pytest.raises(ProcessLookupError):
+            os.kill(pid, 0)

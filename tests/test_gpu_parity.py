@@ -39,6 +39,15 @@ def decode_subset(nv, shards, keep):
     return E.reconstruct(nv, [(i, shards[i]) for i in range(nv) if i in keep])
 
 
+@pytest.mark.gpu
+def test_checker_is_the_reference(oracle):
+    """Which checker the byte comparisons of this run used:
+    the reference ec-cpp build travels with the tree, so it must be it."""
+    import oracle as orc
+    assert oracle.kind == ("reference" if orc.RefEC.available() else "restatement")
+    print("checker:", oracle.kind)
+
+
 # ---------------------------------------------------------------- reference KATs
 def test_kat_whole_data():  # ReconstructChunksFromWholeData
     sh = E.obtain_chunks(6, TEST_DATA.encode())

@@ -63,6 +63,12 @@ def test_bench_gpus_flag_launches_ranks():
     assert line["config"]["parallelism"] == "dp2" and line["ranks"] == 2, line
     assert line["roundtrip_ok"] and "gloo" in line["rehearsal"], line
     assert line["value"] > 0 and line["steps"] == 2
+    # one entry per rank, distinct ranks, each with its own
+    # step time, and the max of them is the line's ms_per_step
+    det = line["ranks_detail"]
+    assert line["world_size"] == 2 and [d["rank"] for d in det] == [0, 1], det
+    assert all(d["step_ms"] > 0 and d["device"] == 0 for d in det), det  # (both on the box's one GPU)
+    assert max(d["step_ms"] for d in det) <= line["ms_per_step"] * 1.001, (det, line["ms_per_step"])
 
 
 def test_bench_stream_two_ranks_share_gpu():

@@ -241,3 +241,42 @@ def test_bench_scatter_gather_timeout_exits_nonzero():
     for p in procs:
         p.join(timeout=120)
     assert procs[0].exitcode == bench.EXIT_SG_TIMEOUT == 3
+
+
+def _rank_table_worker(rank, world, port, q):
+    """bench.py's per-rank evidence (VERDICT r04 item 7) on gloo: every rank's
+    device_info + own step time, all-gathered in rank order."""
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        info = dict(bench.device_info(rank), rank=rank, step_ms=1.0 + rank)
+        table = sharding.rank_table(info, dist)
+        mx = sharding.max_over_ranks(1.0 + rank, dist)
+        if rank == 0:
+            q.put((table, mx))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rank_table_gloo_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, port = 2, _free_port()
+    procs = [ctx.Process(target=_rank_table_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        table, mx = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert [t["rank"] for t in table] == [0, 1] and [t["device"] for t in table] == [0, 1]
+    assert all(set(t) >= {"rank", "device", "name", "pci_bus_id", "step_ms"} for t in table), table
+    assert mx == max(t["step_ms"] for t in table) == 2.0
+    assert sharding.rank_table({"rank": 0}) == [{"rank": 0}]  # one process: no group needed

@@ -22,6 +22,13 @@ def sha(b):
     return hashlib.sha256(b).hexdigest()
 
 
+
+@pytest.fixture(scope="module")
+def oracle(restatement):
+    """This module pins the C restatement itself (not the Checker the GPU
+    parity tests use): it must equal the reference's goldens on its own."""
+    return restatement
+
 def test_tables_match_reference_golden_header(oracle, golden_tables):
     g = golden_tables
     assert sha(oracle.table("log").tobytes()) == g["header_LOG_TABLE_sha256"]
@@ -177,3 +184,18 @@ def test_bench_gf_mul_counts(oracle, nv, cnt):
     e, r = bench.gf_mul_counts(nv, n, k, cnt)
     assert e == enc
     assert r == pytest.approx(cnt + 2 * rec_fft + k * (1 - cnt / nv))
+
+
+def test_checker_uses_reference_for_bytes(restatement):
+    """the parity tests' byte outputs are checked against
+    the reference ec-cpp itself whenever its build (oracle/_ref) exists; the
+    restatement serves the internals the reference does not export."""
+    chk = orc.Checker.default()
+    if not orc.RefEC.available():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    assert chk.kind == "reference" and chk.encode.__self__ is chk.ref
+    assert chk.error_poly.__self__ is chk.restatement
+    p = bytes(range(256)) * 5 + b"\x07"
+    assert chk.encode(100, p) == restatement.encode(100, p)
+    keep = [s if i % 3 == 0 else None for i, s in enumerate(chk.encode(100, p))]
+    assert chk.reconstruct(100, keep)[:len(p)] == p
