@@ -122,14 +122,17 @@ bool n1024_packed(size_t slen, uintptr_t sh, size_t sstride);
 // payloads or pitches the unpacked kernel cannot take; ..._ok: its own limits
 bool k256_packed(size_t plen, size_t pstride, size_t batch, uintptr_t pay, uintptr_t sh, size_t sstride);
 bool k256_packed_ok(size_t plen, size_t batch, uintptr_t sh, size_t sstride);
+// scratch: k256_scratch_bytes (the n = 1024 unpacked form's tile counter)
 hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
-                              size_t sstride, hipStream_t s);
+                              size_t sstride, void *scratch, hipStream_t s);
+size_t k256_scratch_bytes(const CodeParams &p);
 // the n = 1024, unpacked case of launch_encode_k256: two 8-wave workgroups per
-// CU on the compact image (enc_k256w.hip)
+// CU on the compact image, tiles scheduled dynamically from a counter in
+// `scratch` (enc_k256w.hip)
 hipError_t launch_encode_k256w(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                                size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
-                               size_t sstride, hipStream_t s);
+                               size_t sstride, void *scratch, hipStream_t s);
 
 // specialised kernels (enc_k1024.hip): k = 1024, n = 4096, needs a coefficient
 // scratch of k1024_scratch_bytes

@@ -31,8 +31,9 @@ constexpr int THREADS = 64 * WAVES;
 constexpr int TILE = 8 * WAVES;  // pieces per tile
 constexpr uint32_t XCH_BYTES = 256 * 16;   // per-wave exchange / staging region
 constexpr uint32_t XCH0 = kCImgBytes;      // the regions follow the tables
-constexpr int LDS_BYTES = int(XCH0 + WAVES * XCH_BYTES);
-static_assert(LDS_BYTES == 65536, "two workgroups per CU");
+constexpr uint32_t SLOT = XCH0 + WAVES * XCH_BYTES;  // the next tile's index (dynamic schedule)
+constexpr int LDS_BYTES = int(SLOT + 16);
+static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
 static_assert(kCImgBytes % (16 * THREADS) == 0, "whole image chunks per thread");
 
 // Element index of a stage-m butterfly whose a-position is pos, in a transform
@@ -158,15 +159,24 @@ __device__ __forceinline__ void stage_own8(const State &s, uint8_t *xch, uint32_
 // wave * 8 + lane / 8.  Fast path (uniform): 16-B aligned rows, the whole tile
 // inside the payload, all 256 rows below n_validators -- one streaming 16-B
 // store per lane and row, 8 lanes per 128-B row segment.
+__device__ __forceinline__ bool store_fast(const uint8_t *SH, uint64_t sstride, uint32_t s0, int nv,
+                                           uint64_t piece0, uint64_t npieces) {
+  return ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0 && piece0 + TILE <= npieces &&
+         int(s0) + 256 <= nv;
+}
+
+// `then` runs at the end of each path: code that waits for a load issued
+// before the stores is placed there, so the compiler's wait on the fast path
+// counts its 4 stores (vmcnt(4)) instead of the minimum over every path.
+template <typename Then>
 __device__ __forceinline__ void store_own8(uint8_t *SH, uint64_t sstride, uint32_t s0, int nv,
                                            uint64_t piece0, uint64_t npieces, uint32_t wave,
-                                           uint32_t lane) {
+                                           uint32_t lane, Then &&then) {
   asm volatile("" : "+v"(lane));  // recomputed here, not kept live across the FFTs
   const uint32_t c = lane & 7;
   const uint32_t v0 = wave * 8 + (lane >> 3);
   const uint32_t sa = XCH0 + c * XCH_BYTES + soff8(v0, c);
-  if (((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0 && piece0 + TILE <= npieces &&
-      int(s0) + 256 <= nv) {
+  if (store_fast(SH, sstride, s0, nv, piece0, npieces)) {
     uint8_t *dst = SH + uint64_t(s0 + v0) * sstride + 2 * (piece0 + 8 * c);
     const uint64_t dstep = uint64_t(8 * WAVES) * sstride;
 #pragma unroll
@@ -174,6 +184,8 @@ __device__ __forceinline__ void store_own8(uint8_t *SH, uint64_t sstride, uint32
       const v4u val = lds_r128(sa ^ soff8(uint32_t(it) * 8 * WAVES, 0));
       __builtin_nontemporal_store(val, reinterpret_cast<v4u *>(dst + it * dstep));  // written once
     }
+    then();
+    asm volatile("; store_own8 fast path end" ::: "memory");  // distinct tails: `then` is not merged
     return;
   }
   const uint64_t p = piece0 + 8 * c;
@@ -198,6 +210,23 @@ __device__ __forceinline__ void store_own8(uint8_t *SH, uint64_t sstride, uint32
         *reinterpret_cast<uint16_t *>(dst + 2 * e) = uint16_t(w[e >> 1] >> (16 * (e & 1)));
     }
   }
+  then();
+  asm volatile("; store_own8 slow path end" ::: "memory");
+}
+
+// 4 x 16 payload bytes (4 pieces, positions 8q..8q+7) -> byte-planar State:
+// 4x4 byte transposes, dword j of each piece = (hi_{2j}, lo_{2j}, hi_{2j+1}, lo_{2j+1})
+__device__ __forceinline__ void to_state(const v4u (&d)[4], State &s) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t D0 = d[0][j], D1 = d[1][j], D2 = d[2][j], D3 = d[3][j];
+    const uint32_t t0 = vperm(D1, D0, 0x05010400u), t1 = vperm(D1, D0, 0x07030602u);
+    const uint32_t u0 = vperm(D3, D2, 0x05010400u), u1 = vperm(D3, D2, 0x07030602u);
+    s.h[0][2 * j] = vperm(u0, t0, 0x05040100u);
+    s.l[0][2 * j] = vperm(u0, t0, 0x07060302u);
+    s.h[0][2 * j + 1] = vperm(u1, t1, 0x05040100u);
+    s.l[0][2 * j + 1] = vperm(u1, t1, 0x07060302u);
+  }
 }
 
 }  // namespace
@@ -206,9 +235,12 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k256w(const uint8_t *__rest
                                                            uint64_t plen, uint64_t pstride,
                                                            uint8_t *__restrict__ shards, uint64_t slen,
                                                            uint64_t sstride, int nv, uint32_t batch,
-                                                           const uint8_t *__restrict__ cimg) {
+                                                           const uint8_t *__restrict__ cimg,
+                                                           uint32_t *__restrict__ tick) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid0 = threadIdx.x;
+  auto *slot = reinterpret_cast<__attribute__((address_space(3))) volatile uint32_t *>(uintptr_t(SLOT));
+  if (tid0 == 0) *slot = atomicAdd(tick, 1u);  // this workgroup's first tile
   {  // the compact image (32 KB), every load issued before the first store
     constexpr int kPer = int(kCImgBytes / 16 / THREADS);
     v4u v[kPer];
@@ -221,10 +253,66 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k256w(const uint8_t *__rest
 
   const uint64_t npieces = slen / 2;
   const uint32_t tiles_pp = uint32_t((npieces + TILE - 1) / TILE);
-  const uint64_t total = uint64_t(tiles_pp) * batch;
+  const uint32_t total = tiles_pp * batch;  // < 2^32 (launch_encode_k256w)
   const uint32_t wave_s = __builtin_amdgcn_readfirstlane(tid0 >> 6);
-  TileWalk walk(blockIdx.x, gridDim.x, tiles_pp);
-  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x, walk.advance()) {
+  // Dynamic schedule: tiles are taken from the launch's counter (`tick`,
+  // zeroed before the launch) one tile ahead, so the two workgroups of a CU,
+  // which the issue arbiter serves at unequal rates (the older one's waves win
+  // ties), finish together.  With a static grid-stride split the faster one
+  // ended up to 2.8 ms before the slower one of a 7 ms launch, which then ran
+  // alone (scripts/variants/clk_run.py).
+  // Thread 0 takes tile t + 1 at the start of tile t and publishes it in the
+  // LDS slot after the tile's systematic stores; every wave reads it after the
+  // barrier that follows IFFT pass A; the slot is rewritten only after the
+  // next tile-start barrier, by which every wave has read it.
+  uint32_t cur = __builtin_amdgcn_readfirstlane(*slot);
+
+  // This lane's 4 x 16 payload bytes of tile (b, i): pieces i * TILE + 8 wave +
+  // 4 inst + u, bytes 16 q .. 16 q + 15 of each, zero past plen.  A tile's loads
+  // are issued at the end of the previous tile, before its last row stores, and
+  // turned into the next State right after those stores (store_own8's `then`).
+  // vmcnt counts loads and stores together in issue order: loads issued after
+  // a store phase (the tile start) wait for those stores to complete.
+  v4u d[4];
+  State nxt;  // the next tile's data, byte-planar, symbol coordinates
+  const auto fetch = [&](uint64_t fb, uint64_t fi) __attribute__((always_inline)) {
+    const uint8_t *FP = payloads + fb * pstride;
+    const uint64_t pw = fi * TILE + 8 * wave_s;  // this wave's first piece (uniform)
+    uint32_t ftid = tid0;
+    asm volatile("" : "+v"(ftid));  // per-lane addresses recomputed here, not hoisted and spilled
+    const uint32_t lane = ftid & 63, inst = lane >> 5, q = lane & 31;
+    if ((pw + 8) * 2 * K <= plen) {  // the wave's 8 pieces inside the payload: 4 loads in flight
+      const uint8_t *src = FP + (pw + 4 * inst) * 2 * K + 16 * q;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d[u] = *reinterpret_cast<const v4u *>(src + u * 2 * K);
+    } else if (pw < npieces) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t off = (pw + 4 * inst + u) * 2 * K + 16 * q;
+        uint32_t w[4] = {0, 0, 0, 0};
+        if (off + 16 <= plen) {
+          const v4u x = *reinterpret_cast<const v4u *>(FP + off);
+          w[0] = x.x;
+          w[1] = x.y;
+          w[2] = x.z;
+          w[3] = x.w;
+        } else {
+          for (uint64_t e = off; e < plen && e < off + 16; ++e)
+            w[(e - off) >> 2] |= uint32_t(FP[e]) << (8 * ((e - off) & 3));
+        }
+        d[u] = v4u{w[0], w[1], w[2], w[3]};
+      }
+    } else {  // every path assigns d: the old value is never carried across a tile
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d[u] = v4u{0, 0, 0, 0};
+    }
+  };
+  if (cur < total) {
+    fetch(cur / tiles_pp, cur % tiles_pp);
+    to_state(d, nxt);
+  }
+
+  while (cur < total) {
     // lane ids made opaque per tile: per-lane LDS addresses are recomputed in
     // the loop instead of being hoisted out of it and spilled
     uint32_t tid = tid0;
@@ -236,14 +324,41 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k256w(const uint8_t *__rest
     xb.a = mswz(ulaneA(q, inst));
     xb.b = mswz(ulaneB(q, inst));
     xb.c = mswz(ulaneC(q, inst));
-    const uint64_t b = walk.b, piece0 = walk.i * TILE;
-    const uint8_t *P = payloads + b * pstride;
+    const uint64_t b = cur / tiles_pp, piece0 = uint64_t(cur % tiles_pp) * TILE;
+    uint32_t taken = 0;  // thread 0: the tile taken for after this one
+    if (tid0 == 0) taken = atomicAdd(tick, 1u);
+    uint32_t next = 0;   // every wave: that tile, read from the slot
     uint8_t *SH = shards + b * uint64_t(nv) * sstride;
+    // the last coset of this n_validators (uniform), after whose staging the
+    // next tile's payload is fetched
+    const uint32_t last_sh = nv > 768 ? 768u : 512u;  // nv > 512 (launch_encode_k256w)
+    const auto fetch_next = [&]() __attribute__((always_inline)) {
+      next = __builtin_amdgcn_readfirstlane(*slot);
+      // past the end: the zero path, no loads
+      fetch(next < total ? next / tiles_pp : 0, next < total ? next % tiles_pp : tiles_pp);
+    };
     const auto rsync = [&]() __attribute__((always_inline)) { lds_barrier(); };
     const auto store = [&](uint32_t s0) __attribute__((always_inline)) {
       // the row stores (LDS reads + global stores) at raised issue priority
       __builtin_amdgcn_s_setprio(1);
-      store_own8(SH, sstride, s0, nv, piece0, npieces, wave_s, lane);
+      store_own8(SH, sstride, s0, nv, piece0, npieces, wave_s, lane, [] {});
+      __builtin_amdgcn_s_setprio(0);
+    };
+    // the systematic rows' store phase; thread 0 then publishes the tile it
+    // took (the wait for the atomic's return then counts only the stores
+    // issued after it on the fast path, store_own8)
+    const auto store_sys = [&]() __attribute__((always_inline)) {
+      __builtin_amdgcn_s_setprio(1);
+      store_own8(SH, sstride, 0, nv, piece0, npieces, wave_s, lane, [&]() __attribute__((always_inline)) {
+        if (tid0 == 0) *slot = taken;
+      });
+      __builtin_amdgcn_s_setprio(0);
+    };
+    // the last store phase of the tile, then the next tile's State
+    const auto store_last = [&](uint32_t s0) __attribute__((always_inline)) {
+      __builtin_amdgcn_s_setprio(1);
+      store_own8(SH, sstride, s0, nv, piece0, npieces, wave_s, lane,
+                 [&]() __attribute__((always_inline)) { to_state(d, nxt); });
       __builtin_amdgcn_s_setprio(0);
     };
 
@@ -259,47 +374,26 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k256w(const uint8_t *__rest
       for (uint32_t sh = K; sh < 1024u && int(sh) < nv; sh += K) {
         rsync();  // after pass C
         rsync();  // rows staged
-        store(sh);
+        if (sh == last_sh) {
+          fetch_next();
+          store_last(sh);
+        } else {
+          store(sh);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
+      cur = next;
       continue;
     }
 
-    // ---- load 8 pieces x 16 bytes (positions 8q..8q+7), zero past plen
-    State s;
-    {
-      v4u d[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint64_t piece = piece0 + wave * 8 + inst * 4 + u;
-        const uint64_t off = piece * 2 * K + 16 * q;
-        if (off + 16 <= plen) {
-          d[u] = *reinterpret_cast<const v4u *>(P + off);
-        } else {
-          uint32_t w[4] = {0, 0, 0, 0};
-          for (uint64_t e = off; e < plen && e < off + 16; ++e)
-            w[(e - off) >> 2] |= uint32_t(P[e]) << (8 * ((e - off) & 3));
-          d[u] = v4u{w[0], w[1], w[2], w[3]};
-        }
-      }
-      // 4x4 byte transposes: dword j of each piece = (hi_{2j}, lo_{2j}, hi_{2j+1}, lo_{2j+1})
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t D0 = d[0][j], D1 = d[1][j], D2 = d[2][j], D3 = d[3][j];
-        const uint32_t t0 = vperm(D1, D0, 0x05010400u), t1 = vperm(D1, D0, 0x07030602u);
-        const uint32_t u0 = vperm(D3, D2, 0x05010400u), u1 = vperm(D3, D2, 0x07030602u);
-        s.h[0][2 * j] = vperm(u0, t0, 0x05040100u);
-        s.l[0][2 * j] = vperm(u0, t0, 0x07060302u);
-        s.h[0][2 * j + 1] = vperm(u1, t1, 0x05040100u);
-        s.l[0][2 * j + 1] = vperm(u1, t1, 0x07060302u);
-      }
-    }
+    // ---- 8 pieces x 16 bytes (positions 8q..8q+7), fetched by the previous tile
+    State s = nxt;
 
     // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)
     rsync();  // the other waves are done reading this region (last tile)
     stage_own8(s, xch, q, inst, wave);
     rsync();
-    store(0);
+    store_sys();
     __builtin_amdgcn_sched_barrier(0);
     {  // into tower coordinates
       const TowerK tk = tower_k();
@@ -319,7 +413,7 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k256w(const uint8_t *__rest
     // ---- FFT_256 at each coset shift (encodeLow, poly_encoder.hpp:229-237).
     // Kinds of pass A's stages 2 / 1 / 0 by coset: 256: sub / sub / F9;
     // 512, 768: sub / F9 / general (x = (pos + off) >> (m + 1), ec_kernels.hpp)
-    const auto coset = [&](auto t1, auto t0, const uint32_t off) __attribute__((always_inline)) {
+    const auto coset = [&](auto t1, auto t0, const uint32_t off, auto last) __attribute__((always_inline)) {
       using T1 = decltype(t1);
       using T0 = decltype(t0);
       // coef made opaque in place (no copy): keeps the compiler from hoisting
@@ -338,30 +432,43 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k256w(const uint8_t *__rest
         for (int r = 0; r < 8; ++r) s.l[0][r] = tower_lo(s.l[0][r], s.h[0][r], tk);
       }
       stage_own8(s, xch, q, inst, wave);
+      if constexpr (decltype(last)::value) fetch_next();  // coef and s are dead here
       rsync();
-      store(off);
+      if constexpr (decltype(last)::value)
+        store_last(off);
+      else
+        store(off);
       __builtin_amdgcn_sched_barrier(0);
     };
-    coset(SubTab(), F9Tab(), K);  // (nv > 256 for k = 256)
-    for (uint32_t sh = 2 * K; sh < 1024u && int(sh) < nv; sh += K) coset(F9Tab(), Tab(), sh);
+    // n_validators 766..1024 (k = 256, n = 1024): cosets 256, 512 and, above
+    // 768, 768; the last one has its own body (it fetches the next tile)
+    coset(SubTab(), F9Tab(), K, std::false_type());
+    if (last_sh == 3 * K) coset(F9Tab(), Tab(), 2 * K, std::false_type());
+    coset(F9Tab(), Tab(), last_sh, std::true_type());
+    cur = next;
   }
 }
 
 hipError_t launch_encode_k256w(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                                size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
-                               size_t sstride, hipStream_t s) {
+                               size_t sstride, void *scratch, hipStream_t s) {
   int cus = 0;
   if (!t.cimg) return hipErrorInvalidValue;
   if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&encode_k256w), LDS_BYTES, &cus);
       e != hipSuccess)
     return e;
+  if (p.nv <= 2 * K || p.nv > 1024) return hipErrorInvalidValue;  // cosets 256, 512 (, 768)
   const size_t sl = shard_len(p.k, plen);
   const size_t tiles = (sl / 2 + TILE - 1) / TILE * batch;
+  if (!scratch || tiles >= (size_t(1) << 32) - size_t(4) * cus) return hipErrorInvalidValue;
+  // the tile counter (k256w_scratch_bytes), zeroed in stream order
+  uint32_t *tick = static_cast<uint32_t *>(scratch);
+  if (const hipError_t e = hipMemsetAsync(tick, 0, sizeof(uint32_t), s); e != hipSuccess) return e;
   const size_t slots = 2 * size_t(cus);  // two workgroups per CU
   const unsigned grid = unsigned(tiles < slots ? tiles : slots);
   hipLaunchKernelGGL(encode_k256w, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads, uint64_t(plen),
                      uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride), int(p.nv),
-                     uint32_t(batch), t.cimg);
+                     uint32_t(batch), t.cimg, tick);
   return hipGetLastError();
 }
 

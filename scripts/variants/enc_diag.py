@@ -14,6 +14,8 @@ that work costs in the real interleaving:
     notab   multiply tables from VALU-derived words instead of LDS reads
     cmp     nobar + nost + nold: the transforms alone
     cmpt    cmp + notab: the register-only instruction stream
+    dclk    the clk probe in reconstruct_n1024 instead (writes OUTDIR/dec_n1024.hip;
+            clk_run.py dec)
     clk     wave 0 of every workgroup sums s_memtime (shader clock) and
             s_memrealtime (100 MHz) over its lifetime: the clock under load
             (scripts/variants/clk_run.py); combine as e.g. clk+nostg
@@ -28,6 +30,7 @@ kind, out = sys.argv[1], sys.argv[2]
 os.makedirs(out, exist_ok=True)
 enc = open(f"{CS}/enc_k256w.hip").read()
 cim = open(f"{CS}/cimg.hpp").read()
+dec = open(f"{CS}/dec_n1024.hip").read()
 
 
 READER = '''
@@ -42,6 +45,17 @@ extern "C" int ECCR_DIAG_stamps(unsigned long long *out, int n, int reset) {
   return n;
 }
 '''
+
+
+CLK_END = ("  if (threadIdx.x == 0) {\n"
+           "    atomicAdd(&g_stamp[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - clk_t0));\n"
+           "    atomicAdd(&g_stamp[1], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - clk_r0));\n"
+           "    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();\n"
+           "    atomicMin(&g_stamp[2], (unsigned long long)clk_r0);\n"
+           "    atomicMax(&g_stamp[3], (unsigned long long)clk_r0);\n"
+           "    atomicMin(&g_stamp[4], r1);\n"
+           "    atomicMax(&g_stamp[5], r1);\n"
+           "    atomicAdd(&g_stamp[6], 1ull);\n  }\n")
 
 
 def rep(s, old, new):
@@ -71,18 +85,16 @@ for k in kinds:
         enc = rep(enc, "  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];\n",
                   "  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];\n"
                   "  const uint64_t clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();\n")
-        enc = rep(enc, "  }\n}\n\nhipError_t launch_encode_k256w",
-                  "  }\n  if (threadIdx.x == 0) {\n"
-                  "    atomicAdd(&g_stamp[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - clk_t0));\n"
-                  "    atomicAdd(&g_stamp[1], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - clk_r0));\n"
-                  "    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();\n"
-                  "    atomicMin(&g_stamp[2], (unsigned long long)clk_r0);\n"
-                  "    atomicMax(&g_stamp[3], (unsigned long long)clk_r0);\n"
-                  "    atomicMin(&g_stamp[4], r1);\n"
-                  "    atomicMax(&g_stamp[5], r1);\n"
-                  "    atomicAdd(&g_stamp[6], 1ull);\n  }\n"
-                  "}\n\nhipError_t launch_encode_k256w")
+        enc = rep(enc, "  }\n}\n\nhipError_t launch_encode_k256w", "  }\n" + CLK_END + "}\n\nhipError_t launch_encode_k256w")
         enc += READER
+    elif k == "dclk":
+        dec = rep(dec, "namespace ecamd {\nnamespace {", "namespace ecamd {\n__device__ unsigned long long g_stamp[16];\nnamespace {")
+        dec = rep(dec, "  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];\n  uint8_t *tabs = lds;\n",
+                  "  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];\n  uint8_t *tabs = lds;\n"
+                  "  const uint64_t clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();\n")
+        dec = rep(dec, "    __builtin_amdgcn_s_setprio(0);  // the next tile's gather: equal\n  }\n}\n",
+                  "    __builtin_amdgcn_s_setprio(0);  // the next tile's gather: equal\n  }\n" + CLK_END + "}\n")
+        dec += READER
     elif k == "nold":
         enc = rep(enc, "      for (int u = 0; u < 4; ++u) d[u] = *reinterpret_cast<const v4u *>(src + u * 2 * K);\n",
                   "      for (int u = 0; u < 4; ++u) d[u] = v4u{uint32_t(pw) * 0x9E3779B1u + u, uint32_t(fb) ^ 0x5bd1e995u, q * 77u, inst};\n")
@@ -98,4 +110,5 @@ for k in kinds:
         raise SystemExit(f"unknown kind {k}")
 open(f"{out}/enc_k256w.hip", "w").write(enc)
 open(f"{out}/cimg.hpp", "w").write(cim)
+open(f"{out}/dec_n1024.hip", "w").write(dec)
 print("wrote", out, kinds)

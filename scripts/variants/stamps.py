@@ -80,8 +80,8 @@ elif kind == "encw":
     s = rep(s, "    const auto rsync = [&]() __attribute__((always_inline)) { lds_barrier(); };",
             "    const auto rsync = [&]() __attribute__((always_inline)) { STAMP(3); lds_barrier(); STAMP(1); };")
     # both store lambdas (store, store_last)
-    s = rep(s, "      __builtin_amdgcn_s_setprio(1);\n", "      STAMP(3);\n      __builtin_amdgcn_s_setprio(1);\n", 2)
-    s = rep(s, "      __builtin_amdgcn_s_setprio(0);\n    };", "      __builtin_amdgcn_s_setprio(0);\n      STAMP(2);\n    };", 2)
+    s = rep(s, "      __builtin_amdgcn_s_setprio(1);\n", "      STAMP(3);\n      __builtin_amdgcn_s_setprio(1);\n", 3)
+    s = rep(s, "      __builtin_amdgcn_s_setprio(0);\n    };", "      __builtin_amdgcn_s_setprio(0);\n      STAMP(2);\n    };", 3)
     s = rep(s, "    // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)\n",
             "    STAMP(0);\n    // ---- systematic shards 0..255 = the data symbols (poly_encoder.hpp:239)\n")
     s = rep(s, "  }\n}\n\nhipError_t launch_encode_k256w", "  }\n" + FLUSH + "}\n\nhipError_t launch_encode_k256w")
