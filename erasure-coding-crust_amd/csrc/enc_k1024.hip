@@ -6,14 +6,18 @@
 // skews (80 KB of multiply tables).  All 4095 tables do not fit LDS next to the
 // exchange regions, so one persistent launch cycles the four table sets
 // through LDS per tile (LDS-DMA, hidden behind shard stores; see the kernel).
-// (Until round 3: one launch per transform with the coefficients round-tripped
-// through HBM)
 //
-// Tile = 64 consecutive pieces (piece = 2048 payload bytes = 1024 symbols);
-// wave w owns pieces [8w, 8w + 8) as two byte-planar groups of 4, each run
-// through tf1024.hpp's register passes.  Shard rows (128 B per row per tile)
-// are staged in two halves of 512 rows through the waves' own regions and
-// stored as 16 B per lane, 128-B row segments.
+// Tile = 32 consecutive pieces (piece = 2048 payload bytes = 1024 symbols);
+// wave w owns pieces [4w, 4w + 4) as ONE byte-planar group, run through
+// tf1024.hpp's register passes.  The IFFT coefficients stay in registers for
+// every coset (round 5: until then two groups per wave and a 64-piece tile,
+// with the coefficients of cosets 2 and 3 read back from a per-workgroup L2
+// scratch slot: 1.59x the algorithmic HBM traffic).
+// Shard rows (64 B per row per tile) are staged in the waves' own regions,
+// 8 B per row, and stored as 16 B per lane from two adjacent regions.
+// Tiles are taken from a per-launch counter (dynamic schedule: the static
+// grid-stride split gave every 8th workgroup all the payloads' partial last
+// tiles, so they ended ~10% apart).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,72 +33,72 @@ using namespace tf;
 constexpr int K = 1024;
 constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
-constexpr int TILE = 8 * WAVES;  // pieces
-constexpr int LDS_BYTES = Tabs::kBytes + WAVES * REG_BYTES;
+constexpr int TILE = 4 * WAVES;  // pieces: one byte-planar group per wave
+constexpr uint32_t SLOT = Tabs::kBytes + WAVES * REG_BYTES;  // the next tile's index
+constexpr int LDS_BYTES = int(SLOT + 16);
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
-constexpr size_t SCRATCH_PER_WG = size_t(WAVES) * 2 * 16 * 64 * sizeof(uint2);  // a tile's coefficients
-constexpr size_t kMaxGrid = 1024;  // workgroups of the launch (>= the CU count)
 
-// own-region staging slot of row v (0..511) of wave w: the 8 lanes reading one
-// row from the 8 regions hit 8 distinct 16-B slots
-__host__ __device__ constexpr uint32_t soff(uint32_t v, uint32_t w) {
-  return ((v >> 4) << 8) | (((v ^ (v >> 4) ^ w) & 15) << 4);
+// global stores per lane of store_rows' fast path: the hand-written
+// s_waitcnt vmcnt(kStoreIts) in the kernel rely on it (tests/test_asm_checks.py
+// counts them in the built code)
+constexpr int kStoreIts = 1024 / (16 * WAVES);
+static_assert(kStoreIts == 8, "the vmcnt(8) waits below");
+
+// own-region staging slot of row v (0..1023), 8 B: the store reads (lane =
+// row-in-16 << 2 | 16-B chunk c = regions 2c, 2c + 1) spread over the banks
+__host__ __device__ constexpr uint32_t soff(uint32_t v) {
+  return ((v >> 5) << 8) | (((v ^ (v >> 5)) & 31) << 3);
 }
 
-// rows 16 (lane & 31) + r of the lanes of half hf -> own region (16 B: groups 0, 1)
-__device__ __forceinline__ void stage_half(const S16 &g0, const S16 &g1, uint8_t *my,
-                                           uint32_t lane, uint32_t wave, uint32_t hf) {
-  if ((lane >> 5) != hf) return;
+// row v of this wave's group -> own region (8 B, big-endian symbols of its 4 pieces)
+__device__ __forceinline__ void stage_rows(const S16 &g, uint8_t *my, uint32_t lane) {
+  // layout A: position 16 lane + r
+  const uint32_t a = lds_addr(my);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const uint2 a = to_be(g0.l[r], g0.h[r]), b = to_be(g1.l[r], g1.h[r]);
-    *reinterpret_cast<uint4 *>(my + soff(16 * (lane & 31) + uint32_t(r), wave)) =
-        make_uint4(a.x, a.y, b.x, b.y);
-  }
+  for (int r = 0; r < 16; ++r) lds_st2(a + soff(16 * lane + uint32_t(r)), to_be(g.l[r], g.h[r]));
 }
 
-// all waves: 512 staged rows -> shards row0 + v; lane = (row-in-8, source wave c)
-__device__ __forceinline__ void store_half(const uint8_t *regions, uint8_t *SH, uint64_t sstride,
+// all waves: the 1024 staged rows -> shards row0 + v (rows >= nv skipped);
+// lane = (row-in-16, chunk c): 16 B = the 8 B of regions 2c and 2c + 1
+__device__ __forceinline__ void store_rows(const uint8_t *regions, uint8_t *SH, uint64_t sstride,
                                            uint32_t row0, int nv, uint64_t piece0,
                                            uint64_t npieces, uint32_t wave, uint32_t lane) {
-  const uint32_t c = lane & 7;
+  asm volatile("" : "+v"(lane));  // recomputed here, not kept live across the FFTs
+  const uint32_t c = lane & 3, vl = wave * 16 + (lane >> 2);
+  const uint32_t ra = lds_addr(regions) + 2 * c * REG_BYTES;
   const uint64_t p = piece0 + 8 * c;
   const bool wide = ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0;  // 16-B aligned rows
-  const uint8_t *src = regions + c * REG_BYTES;
   // the common case, decided once (uniform): aligned rows, the whole tile inside
-  // the payload, all 512 rows below n_validators -- one aligned 16-B store per
-  // lane and row, no per-lane tests (the general loop below compiles to a 4-B +
-  // a misaligned 12-B store per chunk)
-  if (wide && piece0 + TILE <= npieces && int(row0) + 512 <= nv) {
-    const uint32_t v0 = wave * 8 + (lane >> 3);
-    const uint32_t sa = lds_addr(src) + soff(v0, c);
-    uint8_t *dst = SH + uint64_t(row0 + v0) * sstride + 2 * p;
-    const uint64_t dstep = uint64_t(8 * WAVES) * sstride;
+  // the payload, all 1024 rows below n_validators
+  if (wide && piece0 + TILE <= npieces && int(row0) + 1024 <= nv) {
+    uint8_t *dst = SH + uint64_t(row0 + vl) * sstride + 2 * p;
+    const uint64_t dstep = uint64_t(16 * WAVES) * sstride;
 #pragma unroll
-    for (int it = 0; it < 512 / (8 * WAVES); ++it) {  // soff is GF(2)-linear in v = it * 8 WAVES | v0
+    for (int it = 0; it < 1024 / (16 * WAVES); ++it) {  // soff is GF(2)-linear in v = it * 128 | vl
+      const uint32_t o = soff(uint32_t(it) * 16 * WAVES) ^ soff(vl);
+      const uint2 x = lds_ld2(ra + o), y = lds_ld2(ra + REG_BYTES + o);
       typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-      const v4u val = *(const __attribute__((address_space(3))) v4u *)(uintptr_t(sa ^ soff(uint32_t(it) * 8 * WAVES, 0)));
       // streaming (non-temporal): rows are written once, not re-read
-      __builtin_nontemporal_store(val, reinterpret_cast<v4u *>(dst + it * dstep));
+      __builtin_nontemporal_store(v4u{x.x, x.y, y.x, y.y}, reinterpret_cast<v4u *>(dst + it * dstep));
     }
     return;
   }
 #pragma unroll 2
-  for (int it = 0; it < 512 / (8 * WAVES); ++it) {
-    const uint32_t v = uint32_t(it) * 8 * WAVES + wave * 8 + (lane >> 3);
-    const uint4 val = *reinterpret_cast<const uint4 *>(src + soff(v, c));
+  for (int it = 0; it < 1024 / (16 * WAVES); ++it) {
+    const uint32_t v = uint32_t(it) * 16 * WAVES + vl;
+    const uint2 x = lds_ld2(ra + soff(v)), y = lds_ld2(ra + REG_BYTES + soff(v));
     const uint32_t shard = row0 + v;
     if (int(shard) >= nv) continue;
     uint8_t *dst = SH + uint64_t(shard) * sstride + 2 * p;
+    const uint32_t w[4] = {x.x, x.y, y.x, y.y};
     if (p + 8 <= npieces) {
       if (wide) {
-        *reinterpret_cast<uint4 *>(dst) = val;
+        *reinterpret_cast<uint4 *>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
       } else {
-        reinterpret_cast<uint2 *>(dst)[0] = make_uint2(val.x, val.y);
-        reinterpret_cast<uint2 *>(dst)[1] = make_uint2(val.z, val.w);
+        reinterpret_cast<uint2 *>(dst)[0] = make_uint2(w[0], w[1]);
+        reinterpret_cast<uint2 *>(dst)[1] = make_uint2(w[2], w[3]);
       }
     } else if (p < npieces) {
-      const uint32_t w[4] = {val.x, val.y, val.z, val.w};
       for (uint64_t e = 0; e < npieces - p; ++e)
         *reinterpret_cast<uint16_t *>(dst + 2 * e) = uint16_t(w[e >> 1] >> (16 * (e & 1)));
     }
@@ -133,41 +137,30 @@ __device__ __forceinline__ void load_group(S16 &s, const uint8_t *P, uint64_t pl
   }
 }
 
-// symbol <-> tower coordinates of both groups (an involution)
-__device__ __forceinline__ void to_tower(S16 &g0, S16 &g1) {
+// symbol <-> tower coordinates (an involution)
+__device__ __forceinline__ void to_tower(S16 &g) {
   const TowerK tk = tower_k();
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    g0.l[r] = tower_lo(g0.l[r], g0.h[r], tk);
-    g1.l[r] = tower_lo(g1.l[r], g1.h[r], tk);
-  }
-}
-
-// workgroup wg's coefficient slot, wave w, group g: 16 registers x 64 lanes
-__device__ __forceinline__ uint2 *coef_at(uint2 *scratch, uint64_t wg, uint32_t wave, int g) {
-  return scratch + ((wg * WAVES + wave) * 2 + uint64_t(g)) * (16 * 64);
+  for (int r = 0; r < 16; ++r) g.l[r] = tower_lo(g.l[r], g.h[r], tk);
 }
 
 // One persistent launch for all four transforms.  The four 80 KB table sets
-// take turns in LDS, loaded by LDS-DMA: coset 2's, coset 3's and the next
-// tile's index-0 set behind the previous coset's shard stores (its tables are
-// no longer read by then), coset 1's right after the IFFT.  Coset 1 takes the
-// IFFT coefficients from the registers; cosets 2 and 3 read them back from a
-// per-workgroup scratch slot (128 KB, rewritten every tile, so it stays in L2
-// / the memory-side cache).  (Prefetching them behind the previous coset's
-// stores needs 64 more VGPRs at the 256 limit: 15 spills, 7.61 vs 6.95 ms.)
+// take turns in LDS, loaded by LDS-DMA: each coset's set and the next tile's
+// index-0 set as soon as every wave is past the previous transform, behind
+// that coset's shard stores.
 __global__ void __launch_bounds__(THREADS)
     encode_k1024_fused(const uint8_t *__restrict__ payloads, uint64_t plen, uint64_t pstride,
                        uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride, int nv,
-                       uint32_t batch, uint2 *__restrict__ coef, DevTables t) {
+                       uint32_t batch, uint32_t *__restrict__ tick, DevTables t) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
   uint8_t *regions = lds + Tabs::kBytes;
   const uint32_t tid0 = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid0 >> 6);
   uint8_t *my = regions + wave * REG_BYTES;
+  auto *slot = reinterpret_cast<__attribute__((address_space(3))) volatile uint32_t *>(uintptr_t(SLOT));
+  if (tid0 == 0) *slot = atomicAdd(tick, 1u);  // this workgroup's first tile
   // cosets 1 .. ncos - 1 start below n_validators (poly_encoder.hpp:229-236)
   const uint32_t ncos = uint32_t(nv + K - 1) / K;
-  uint2 *const cw0 = coef_at(coef, blockIdx.x, wave, 0), *const cw1 = coef_at(coef, blockIdx.x, wave, 1);
 
   // tower images: the transforms run in tower coordinates
   Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);  // index 0 (the IFFT)
@@ -175,91 +168,86 @@ __global__ void __launch_bounds__(THREADS)
 
   const uint64_t npieces = slen / 2;
   const uint32_t tiles_pp = uint32_t((npieces + TILE - 1) / TILE);
-  const uint64_t total = uint64_t(tiles_pp) * batch;
-  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+  const uint32_t total = tiles_pp * batch;  // < 2^32 (launch_encode_k1024)
+  // thread 0 takes the tile after this one at the tile start and publishes it
+  // in the slot after the first barrier that follows its return; every wave
+  // reads it after the next barrier; the slot is rewritten only in the next
+  // tile, after its start barrier
+  uint32_t cur = __builtin_amdgcn_readfirstlane(*slot);
+  while (cur < total) {
     uint32_t tid = tid0;
     asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63;
-    const uint64_t b = tile / tiles_pp;
-    const uint64_t piece0 = (tile % tiles_pp) * TILE;
+    const uint64_t b = cur / tiles_pp;
+    const uint64_t piece0 = uint64_t(cur % tiles_pp) * TILE;
+    uint32_t taken = 0;
+    if (tid0 == 0) taken = atomicAdd(tick, 1u);
     uint8_t *SH = shards + b * uint64_t(nv) * sstride;
     const uint8_t *P = payloads + b * pstride;
-    S16 g0, g1;
-    // a wave none of whose 8 pieces exist (the payload's last, partial tile:
-    // 1 MB is 489 pieces, its 8th tile has 41) skips its transforms and only
+    S16 g, coef;
+    // a wave none of whose 4 pieces exist (the payload's last, partial tile:
+    // 1 MB is 489 pieces, its 16th tile has 9) skips its transforms and only
     // joins the barriers, the table DMAs and the row stores (uniform)
-    const bool idle = piece0 + 8 * wave >= npieces;
-    const auto load_coef = [&]() __attribute__((always_inline)) {
-      // opaque addresses: the values stored after the IFFT must be read back,
-      // not forwarded from the registers (which would stay live meanwhile)
-      const uint2 *r0 = cw0, *r1 = cw1;
-      asm volatile("" : "+s"(r0), "+s"(r1));
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const uint2 x = r0[r * 64 + lane], y = r1[r * 64 + lane];
-        g0.l[r] = x.x;
-        g0.h[r] = x.y;
-        g1.l[r] = y.x;
-        g1.h[r] = y.y;
-      }
-    };
-    if (!idle) {
-      load_group(g0, P, plen, piece0 + 8 * wave, lane);
-      load_group(g1, P, plen, piece0 + 8 * wave + 4, lane);
-    }
+    const bool idle = piece0 + 4 * wave >= npieces;
+    if (!idle) load_group(g, P, plen, piece0 + 4 * wave, lane);
     // systematic shards 0..1023 = the data symbols (poly_encoder.hpp:239)
-#pragma unroll
-    for (uint32_t hf = 0; hf < 2; ++hf) {
-      lds_barrier();  // the other waves are done reading the regions
-      if (!idle) stage_half(g0, g1, my, lane, wave, hf);
-      lds_barrier();
-      store_half(regions, SH, sstride, 512 * hf, nv, piece0, npieces, wave, lane);
-    }
-    // the index-0 tables (the last tile's DMA, issued before the 16 fast-form
-    // systematic stores just made) landed; the regions are free
-    if (((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0 && piece0 + TILE <= npieces)
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    lds_barrier();  // the other waves are done reading the regions
+    if (!idle) stage_rows(g, my, lane);
+    lds_barrier();
+    store_rows(regions, SH, sstride, 0, nv, piece0, npieces, wave, lane);
+    // the index-0 tables (the last tile's DMA, issued before the systematic
+    // stores just made: 8 per lane on the fast path, kStoreIts) landed; the
+    // regions are free
+    const bool fast_rows = ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0 && piece0 + TILE <= npieces;
+    if (fast_rows && K <= nv)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
     if (!idle) {
-      to_tower(g0, g1);
-      ifft1024<true, tower_sub_min(0)>(g0, tabs, my, lane);
-      ifft1024<true, tower_sub_min(0)>(g1, tabs, my, lane);
+      to_tower(g);
+      ifft1024<true, tower_sub_min(0)>(g, tabs, my, lane);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {  // read back by cosets 2 and 3 (coset 1 uses the registers)
-        cw0[r * 64 + lane] = make_uint2(g0.l[r], g0.h[r]);
-        cw1[r * 64 + lane] = make_uint2(g1.l[r], g1.h[r]);
+      for (int r = 0; r < 16; ++r) {  // the coefficients of every coset, kept in registers
+        coef.l[r] = g.l[r];
+        coef.h[r] = g.h[r];
       }
     }
+    if (tid0 == 0) *slot = taken;  // (issued at the tile start: long returned)
     lds_barrier();  // every wave is done with the index-0 tables
+    const uint32_t next = __builtin_amdgcn_readfirstlane(*slot);
     Tabs::dma_image<THREADS>(tabs, t.timg_t + kTabImageBytes, tid);
     // cs: std::integral_constant coset number (its image's subfield stages)
-    const bool fast_rows = ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0 && piece0 + TILE <= npieces;
     const auto coset = [&](auto cs) __attribute__((always_inline)) {
       constexpr uint32_t s = decltype(cs)::value;
+      // coset s's tables landed (all waves' slices; issued before the previous
+      // coset's row stores, 8 per lane on the fast path) and the regions are free
       if (s > 1 && fast_rows && int(s * K) <= nv) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // coset s's tables and coefficients landed
-      lds_barrier();  // (all waves' slices) and the regions are free
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
       if (!idle) {
-        fft1024<false, tower_sub_min(int(s))>(g0, tabs, my, lane);
-        fft1024<false, tower_sub_min(int(s))>(g1, tabs, my, lane);
-        to_tower(g0, g1);  // back to symbol coordinates
-      }
+        if constexpr (s > 1) {
+          // coef made opaque: copied here, not re-associated into the FFT
 #pragma unroll
-      for (uint32_t hf = 0; hf < 2; ++hf) {
-        if (hf) lds_barrier();
-        if (!idle) stage_half(g0, g1, my, lane, wave, hf);
-        lds_barrier();
-        if (hf == 0)  // every wave is past its FFT: the next set (index 0 after the last coset)
-          Tabs::dma_image<THREADS>(tabs, t.timg_t + (s + 1 < ncos ? s + 1 : 0) * kTabImageBytes, tid);
-        if (hf == 1 && s + 1 < ncos && !idle) load_coef();  // g0 / g1 are staged
-        store_half(regions, SH, sstride, s * K + 512 * hf, nv, piece0, npieces, wave, lane);
+          for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(coef.l[r]), "+v"(coef.h[r]));
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            g.l[r] = coef.l[r];
+            g.h[r] = coef.h[r];
+          }
+        }
+        fft1024<false, tower_sub_min(int(s))>(g, tabs, my, lane);
+        to_tower(g);  // back to symbol coordinates
+        stage_rows(g, my, lane);
       }
+      lds_barrier();  // every wave is past its FFT and staged: the next set (index 0 after the last coset)
+      Tabs::dma_image<THREADS>(tabs, t.timg_t + (s + 1 < ncos ? s + 1 : 0) * kTabImageBytes, tid);
+      store_rows(regions, SH, sstride, s * K, nv, piece0, npieces, wave, lane);
     };
     coset(std::integral_constant<uint32_t, 1>());
     coset(std::integral_constant<uint32_t, 2>());
     if (ncos > 3) coset(std::integral_constant<uint32_t, 3>());
+    cur = next;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
 }
@@ -268,10 +256,7 @@ __global__ void __launch_bounds__(THREADS)
 
 bool k1024_applicable(const CodeParams &p) { return p.k == 1024 && p.n == 4096; }
 
-size_t k1024_scratch_bytes(size_t plen, size_t batch) {
-  const size_t tiles = (shard_len(K, plen) / 2 + TILE - 1) / TILE * batch;
-  return std::min(tiles, kMaxGrid) * SCRATCH_PER_WG;  // one coefficient slot per workgroup
-}
+size_t k1024_scratch_bytes(size_t, size_t) { return 256; }  // the tile counter
 
 hipError_t launch_encode_k1024(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                                size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
@@ -282,11 +267,13 @@ hipError_t launch_encode_k1024(const CodeParams &p, const DevTables &t, const ui
   if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&encode_k1024_fused), LDS_BYTES, &cus);
       e != hipSuccess)
     return e;
-  const unsigned grid = unsigned(std::min({tiles, size_t(cus), kMaxGrid}));
-  if (!scratch) return hipErrorInvalidValue;
+  if (!scratch || tiles >= (size_t(1) << 32) - size_t(2) * cus) return hipErrorInvalidValue;
+  uint32_t *tick = static_cast<uint32_t *>(scratch);
+  if (const hipError_t e = hipMemsetAsync(tick, 0, sizeof(uint32_t), s); e != hipSuccess) return e;
+  const unsigned grid = unsigned(std::min(tiles, size_t(cus)));
   hipLaunchKernelGGL(encode_k1024_fused, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
                      uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride),
-                     int(p.nv), uint32_t(batch), static_cast<uint2 *>(scratch), t);
+                     int(p.nv), uint32_t(batch), tick, t);
   return hipGetLastError();
 }
 

@@ -4,7 +4,8 @@
 (nv = 1024) and prints the summed s_memtime / s_memrealtime ratio of the
 workgroups' wave 0 (GHz), the mean kernel time (HIP events), and for one more
 launch the spread of the workgroups' start and end times.
-usage: ECC_AMD_LIB=... clk_run.py [enc|dec] [B] [ITERS]"""
+usage: ECC_AMD_LIB=... clk_run.py [enc|dec|step] [B] [ITERS]  (step: encode + locator +
+reconstruct per iteration, the reconstruct probed: a dclk variant)"""
 import ctypes as C
 import os
 import sys
@@ -17,7 +18,7 @@ import synth  # noqa: E402
 kind = sys.argv[1] if len(sys.argv) > 1 else "enc"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 iters = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-nv, plen = 1024, 1_000_000
+nv, plen = int(os.environ.get("NV", "1024")), 1_000_000
 n, k, thr = E.code_params(nv)
 sl = E.shard_len(nv, plen)
 ss = (sl + 63) // 64 * 64
@@ -35,9 +36,11 @@ buf = (C.c_ulonglong * 16)()
 
 
 def run():
-    if kind == "enc":
+    if kind in ("enc", "step"):
         E.encode_batch(nv, d_pay, plen, plen, B, d_sh, ss)
-    else:
+    if kind == "step":  # the bench step: the probed reconstruct right after an encode
+        E.error_locator(nv, d_pr, B, d_el)
+    if kind in ("dec", "step"):
         E.reconstruct_batch(nv, d_sh, sl, ss, d_pr, d_el, B, d_out, sl * k)
 
 
@@ -56,7 +59,7 @@ torch.cuda.synchronize()
 L.ECCR_DIAG_stamps(buf, 16, 0)
 ok = kind == "enc" or torch.equal(d_out[:, :plen], d_pay)
 ghz = buf[0] / buf[1] * 0.1 if buf[1] else float("nan")
-print(f"{os.path.basename(os.environ.get('ECC_AMD_LIB', 'main'))} {kind} B={B} {e0.elapsed_time(e1) / iters:.3f} ms"
+print(f"{os.path.basename(os.environ.get('ECC_AMD_LIB', 'main'))} {kind} nv={nv} B={B} {e0.elapsed_time(e1) / iters:.3f} ms"
       f"  shader clock {ghz:.3f} GHz  (memtime {buf[0]}, realtime {buf[1]}, wgs {buf[6]})"
       f"{'' if ok else '  MISMATCH'}")
 # one more launch alone: the spread of workgroup start / end times (realtime ticks, 10 ns)

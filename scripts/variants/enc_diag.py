@@ -14,6 +14,11 @@ that work costs in the real interleaving:
     notab   multiply tables from VALU-derived words instead of LDS reads
     cmp     nobar + nost + nold: the transforms alone
     cmpt    cmp + notab: the register-only instruction stream
+    dnobar  reconstruct_n1024: the two per-tile workgroup barriers dropped
+    dnogat  reconstruct_n1024: the gather's row loads and E[v] multiplies dropped
+    dnoout  reconstruct_n1024: the output stores dropped (values asm-consumed)
+    kclk:F  the clk probe in the kernel of csrc file F (its first kernel with
+            dynamic LDS), e.g. kclk:enc_k1024.hip (writes OUTDIR/F)
     dclk    the clk probe in reconstruct_n1024 instead (writes OUTDIR/dec_n1024.hip;
             clk_run.py dec)
     clk     wave 0 of every workgroup sums s_memtime (shader clock) and
@@ -64,6 +69,7 @@ def rep(s, old, new):
 
 
 ALIAS = {"cmp": ["nobar", "nost", "nold"], "cmpt": ["nobar", "nost", "nold", "notab"]}
+extra = {}
 kinds = [x for part in kind.split("+") for x in ALIAS.get(part, [part])]
 for k in kinds:
     if k == "nobar":
@@ -87,6 +93,32 @@ for k in kinds:
                   "  const uint64_t clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();\n")
         enc = rep(enc, "  }\n}\n\nhipError_t launch_encode_k256w", "  }\n" + CLK_END + "}\n\nhipError_t launch_encode_k256w")
         enc += READER
+    elif k == "dnobar":
+        dec = rep(dec, "    lds_barrier();  // previous tile's readers of the regions are done (LDS only)\n", "")
+        dec = rep(dec, "    if constexpr (!PACKED) __syncthreads();  // packed: the wave's own region and staging only\n", "")
+    elif k == "dnogat":
+        dec = rep(dec, "    if ((meta[0] & 0xffffu) != 0xffffu) load_row(0);\n    lds_barrier();",
+                  "    lds_barrier();")
+        dec = rep(dec, "      if ((meta[half] & 0xffffu) != 0xffffu) {\n", "      if (meta[half] == 0x12345678u) {\n")
+    elif k == "dnoout":
+        dec = rep(dec, "        *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);\n",
+                  "        asm volatile(\"\" :: \"v\"(w0), \"v\"(w1), \"v\"(O + (col * K + 4 * lane) * 2));\n")
+    elif k.startswith("kclk:"):
+        fname = k.split(":", 1)[1]
+        src = open(f"{CS}/{fname}").read()
+        src = rep(src, "namespace ecamd {\nnamespace {", "namespace ecamd {\n__device__ unsigned long long g_stamp[16];\nnamespace {")
+        i = src.index("  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];\n")
+        body = src.rindex("{\n", 0, i) + 2  # the kernel's opening brace
+        j = i + len("  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];\n")
+        depth, e = 1, body
+        while depth:
+            c = src[e]
+            depth += (c == "{") - (c == "}")
+            e += 1
+        close = e - 1  # the kernel's closing brace
+        src = (src[:j] + "  const uint64_t clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();\n"
+               + src[j:close] + CLK_END + src[close:]) + READER
+        extra[fname] = src
     elif k == "dclk":
         dec = rep(dec, "namespace ecamd {\nnamespace {", "namespace ecamd {\n__device__ unsigned long long g_stamp[16];\nnamespace {")
         dec = rep(dec, "  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];\n  uint8_t *tabs = lds;\n",
@@ -111,4 +143,6 @@ for k in kinds:
 open(f"{out}/enc_k256w.hip", "w").write(enc)
 open(f"{out}/cimg.hpp", "w").write(cim)
 open(f"{out}/dec_n1024.hip", "w").write(dec)
+for fname, src in extra.items():
+    open(f"{out}/{fname}", "w").write(src)
 print("wrote", out, kinds)

@@ -1,0 +1,61 @@
+"""Static checks of the built kernel code that hand-written waits rely on
+(ADVICE r04): the encode kernels wait for their table LDS-DMA / payload loads
+with `s_waitcnt vmcnt(N)` counted past the row stores of the fast store path,
+so each fast store phase must issue exactly N global stores per lane.  If a
+toolchain change merged or split those stores, the wait would under-count and
+the transform would read tables still in flight; this catches it.  CPU only:
+compiles the device code to assembly (hipcc -S, gfx950, ~10 s per file)."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "erasure-coding-crust_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+def _asm(name, tmp_path):
+    if not os.path.exists(HIPCC):
+        pytest.skip("no hipcc")
+    out = tmp_path / (name + ".s")
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
+                    "-o", str(out), os.path.join(CSRC, name)], check=True, capture_output=True)
+    return out.read_text()
+
+
+def _nt_store_blocks(text, kernel):
+    """Streaming (nt) global stores per basic block of `kernel` (the fast store
+    paths are the only nt stores)."""
+    lines = text.split("\n")
+    start = next(i for i, l in enumerate(lines) if l.startswith("_Z") and kernel in l.split(":")[0] and ":" in l)
+    counts, cur = [], 0
+    for l in lines[start + 1:]:
+        if re.match(r"^(\.LBB\w+|_Z\w+):", l) or "s_endpgm" in l:
+            if cur:
+                counts.append(cur)
+            cur = 0
+            if "s_endpgm" in l:
+                break
+            continue
+        if re.match(r"\s+global_store_dwordx4 .* nt\b", l):
+            cur += 1
+    return counts
+
+
+def test_enc_k1024_fast_store_count(tmp_path):
+    # enc_k1024.hip: kStoreIts = 8, the vmcnt(8) waits before the IFFT and cosets 2, 3
+    src = open(os.path.join(CSRC, "enc_k1024.hip")).read()
+    assert "kStoreIts == 8" in src and src.count("vmcnt(8)") >= 2
+    blocks = _nt_store_blocks(_asm("enc_k1024.hip", tmp_path), "encode_k1024_fused")
+    assert blocks and all(c == 8 for c in blocks), blocks
+    assert sum(blocks) == 8 * 4, blocks  # systematic rows + 3 cosets
+
+
+def test_enc_k256w_fast_store_count(tmp_path):
+    # enc_k256w.hip: store_own8's fast path, 4 stores per lane; the compiler's
+    # own vmcnt(4) before the next tile's transposes depends on it too
+    blocks = _nt_store_blocks(_asm("enc_k256w.hip", tmp_path), "encode_k256w")
+    assert blocks and all(c == 4 for c in blocks), blocks

@@ -969,9 +969,9 @@ def test_scratch_failure_is_reported(oracle):
     need, as when hipMalloc fails) returns an error and launches nothing;
     with the cap lifted the same calls are bit-exact again."""
     import torch
-    nv, plen = 4096, 30001  # k = 1024 encode keeps its coefficients in scratch
+    nv, plen = 4096, 30001  # the k = 1024 encode takes its tile counter from scratch (256 B)
     p = synth.payload(1, plen).tobytes()
-    E.set_scratch_limit(1024)
+    E.set_scratch_limit(128)
     try:
         with pytest.raises(E.ECError) as e:
             E.obtain_chunks(nv, p)
