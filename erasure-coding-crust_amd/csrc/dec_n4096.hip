@@ -34,7 +34,8 @@ using namespace tf;
 constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
 constexpr int COLS = 4 * WAVES;
-constexpr int LDS_BYTES = Tabs::kBytes + WAVES * REG_BYTES;
+constexpr uint32_t SLOT = Tabs::kBytes + WAVES * REG_BYTES;  // the next tile's index
+constexpr int LDS_BYTES = int(SLOT + 16);
 static_assert(LDS_BYTES <= 160 * 1024 && Tabs::kBytes == kTabImageBytes, "LDS budget");
 
 __device__ __forceinline__ uint32_t mul_index(uint32_t c) { return c == 65535u ? 0u : c; }
@@ -140,7 +141,7 @@ reconstruct_n4096(
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
     const uint32_t *__restrict__ pattern, const uint32_t *__restrict__ order,
     uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t K, uint32_t batch,
-    DevTables t, Lin lin, const uint8_t *__restrict__ oimg) {
+    DevTables t, Lin lin, const uint8_t *__restrict__ oimg, uint32_t *__restrict__ tick) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
   uint8_t *regions = lds + Tabs::kBytes;
@@ -150,8 +151,28 @@ reconstruct_n4096(
   const uint64_t ncols = slen / 2;
   const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);
   const uint64_t total = uint64_t(tiles_pp) * batch;
+  // n = 4096: dynamic XCD-affine schedule (TileQueue; config 4 reconstruct
+  // 7.64 -> 7.37 ms at B = 2048): thread 0 takes the tile after this one at
+  // the tile start and publishes it before the output phase's first barrier;
+  // every wave reads it right after that barrier; the slot is rewritten only
+  // in the next tile, after several barriers.  n = 2048: the static XCD spans
+  // (its shorter tiles ran 2-3% slower dynamically at n_validators 1500)
+  constexpr bool DYN = NQ == 4;
+  const TileQueue tq(uint32_t(total), tick);  // total < 2^32 (launch)
   const TileSpan span = xcd_span(total);
-  for (uint64_t tile = span.first; tile < span.end; tile += span.step) {
+  auto *slot = reinterpret_cast<__attribute__((address_space(3))) volatile uint32_t *>(uintptr_t(SLOT));
+  uint64_t tile = span.first, end = span.end;
+  if constexpr (DYN) {
+    if (tid0 == 0) *slot = tq.take();
+    __syncthreads();
+    tile = __builtin_amdgcn_readfirstlane(*slot);
+    end = tq.hi;
+  }
+  while (tile < end) {
+    uint64_t nxt = tile + span.step;  // (static)
+    uint32_t taken = 0;
+    if constexpr (DYN)
+      if (tid0 == 0) taken = tq.take();
     uint32_t tid = tid0;
     asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63;
@@ -364,7 +385,10 @@ reconstruct_n4096(
 
     // ---- output (decode_main:185-188, reconstructSub:138-149): erased y < k
     // scaled by E[y] (tables now in LDS), present y copied from the shard
+    if constexpr (DYN)
+      if (tid0 == 0) *slot = taken;  // (issued at the tile start: long returned)
     lds_barrier();  // every wave is done with the FFT tables
+    if constexpr (DYN) nxt = __builtin_amdgcn_readfirstlane(*slot);
     // the output tables E[y] from this payload's prebuilt image (n4096_out_image)
     __builtin_amdgcn_sched_barrier(0);
     Tabs::dma_image<THREADS>(tabs, oimg + b * kOutImageBytes, tid);
@@ -393,7 +417,10 @@ reconstruct_n4096(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     lds_barrier();
-    if (idle) continue;
+    if (idle) {
+      tile = nxt;
+      continue;
+    }
     if constexpr (KB < 10) {
       constexpr int SB = swap_rbit<LC>();
       static_assert(regbits_above_lane(), "the output rows' register bits are y bits 7..");
@@ -493,11 +520,12 @@ reconstruct_n4096(
         reinterpret_cast<uint4 *>(dst)[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);
       }
     }
+    tile = nxt;
   }
 }
 
 size_t n4096_scratch_bytes(const CodeParams &p, size_t batch) {
-  return gather_order_bytes(p, batch) + batch * kOutImageBytes;
+  return gather_order_bytes(p, batch) + batch * kOutImageBytes + kTileQueueBytes;
 }
 
 bool n4096_applicable(const CodeParams &p) {  // the (n, k) instantiated below
@@ -526,6 +554,9 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
   hipLaunchKernelGGL(n4096_out_image, dim3(unsigned(batch)), dim3(256), 0, s, d_err_log, d_present, d_pattern,
                        int(p.n), int(p.nv), t.mtab_tout, oimg);  // tower in, symbols out
   const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
+  if (tiles >= (size_t(1) << 32) - size_t(2) * cus) return hipErrorInvalidValue;
+  uint32_t *tick = reinterpret_cast<uint32_t *>(oimg + batch * kOutImageBytes);  // the TileQueue counters
+  if (const hipError_t e = launch_zero_counters(tick, kTileQueueBytes, s); e != hipSuccess) return e;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   static const Lin lin4 = n4096_lin(4), lin2 = n4096_lin(2);
   if (lin4.p[0] == 0xDEAD || lin2.p[0] == 0xDEAD) return hipErrorInvalidValue;  // not subfield (never)
@@ -534,7 +565,7 @@ hipError_t launch_reconstruct_n4096(const CodeParams &p, const DevTables &t,
     hipLaunchKernelGGL((reconstruct_n4096<NQv, KBv>), dim3(grid), dim3(THREADS), LDS_BYTES, s,   \
                        d_shards, uint64_t(slen), uint64_t(sstride), d_present, d_err_log, d_pattern, order, d_out, \
                        uint64_t(ostride), int(p.nv), uint32_t(p.k), uint32_t(batch), t,         \
-                       NQv == 4 ? lin4 : lin2, oimg);
+                       NQv == 4 ? lin4 : lin2, oimg, tick);
   ECAMD_D4(4, 10)
   else ECAMD_D4(4, 9)
   else ECAMD_D4(2, 9)

@@ -109,6 +109,33 @@ __device__ __forceinline__ TileSpan xcd_span(uint64_t total) {
   return {lo + blockIdx.x / 8, g / 8, lo + chunk < total ? lo + chunk : total};
 }
 
+// Dynamic, XCD-affine tile schedule of a persistent grid: the tiles [0, total)
+// are cut into 8 contiguous spans as xcd_span does, span b % 8 served to its
+// group's workgroups from its own counter (zeroed before the launch, 64 B
+// apart), so a payload's tiles stay in one L2 and the workgroups of a group
+// finish together whatever their issue rates.  Grids not a multiple of 8 or
+// small batches: one counter over the whole range.  take() is one atomic; a
+// value >= hi means the span is done.
+constexpr size_t kTileQueueBytes = 8 * 64;
+struct TileQueue {
+  uint32_t lo, hi;
+  uint32_t *ctr;
+  __device__ TileQueue(uint32_t total, uint32_t *ctrs) {
+    const uint32_t g = gridDim.x;
+    if (g % 8 != 0 || total < 8u * g) {
+      lo = 0;
+      hi = total;
+      ctr = ctrs;
+    } else {
+      const uint32_t chunk = (total + 7) / 8, x = blockIdx.x % 8;
+      lo = x * chunk;
+      hi = lo + chunk < total ? lo + chunk : total;
+      ctr = ctrs + 16 * x;
+    }
+  }
+  __device__ __forceinline__ uint32_t take() const { return lo + atomicAdd(ctr, 1u); }
+};
+
 struct Tab {
   uint32_t t[20];
 };

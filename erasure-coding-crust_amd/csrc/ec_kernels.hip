@@ -467,6 +467,19 @@ int groups_for(uint32_t size) {  // byte-planar groups per workgroup
 
 bool locator_wave_applicable(uint32_t n) { return n >= 64 && n <= 4096; }
 
+// zeroes a dynamic schedule's tile counters in stream order.  A kernel, not
+// hipMemsetAsync: a memset captured into a hipGraph did not re-zero the
+// counters on replay here (the reconstruct of the second replay found its
+// queue drained: tests/test_gpu_parity.py test_graph_capture_ws at nv 4096)
+__global__ void zero_words(uint32_t *p, uint32_t n) {
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0;
+}
+
+hipError_t launch_zero_counters(uint32_t *p, size_t bytes, hipStream_t s) {
+  hipLaunchKernelGGL(zero_words, dim3(1), dim3(64), 0, s, p, uint32_t(bytes / 4));
+  return hipGetLastError();
+}
+
 hipError_t launch_signal_host(uint32_t *h_flag, uint32_t v, hipStream_t s) {
   hipLaunchKernelGGL(signal_host, dim3(1), dim3(1), 0, s, h_flag, v);
   return hipGetLastError();

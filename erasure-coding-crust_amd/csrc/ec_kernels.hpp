@@ -96,6 +96,8 @@ hipError_t launch_error_locator(const CodeParams &p, const uint8_t *d_present, s
 bool locator_wave_applicable(uint32_t n);
 // one-lane kernel storing v to a pinned host word (system scope, release)
 hipError_t launch_signal_host(uint32_t *h_flag, uint32_t v, hipStream_t s);
+// zeroes `bytes` (a multiple of 4) of tile counters at p in stream order
+hipError_t launch_zero_counters(uint32_t *p, size_t bytes, hipStream_t s);
 size_t dedup_scratch_bytes(size_t batch);
 hipError_t launch_dedup_patterns(const CodeParams &p, const uint8_t *d_present, size_t batch,
                                  uint32_t *d_pattern, void *scratch, hipStream_t s);

@@ -269,7 +269,7 @@ hipError_t launch_encode_k1024(const CodeParams &p, const DevTables &t, const ui
     return e;
   if (!scratch || tiles >= (size_t(1) << 32) - size_t(2) * cus) return hipErrorInvalidValue;
   uint32_t *tick = static_cast<uint32_t *>(scratch);
-  if (const hipError_t e = hipMemsetAsync(tick, 0, sizeof(uint32_t), s); e != hipSuccess) return e;
+  if (const hipError_t e = launch_zero_counters(tick, sizeof(uint32_t), s); e != hipSuccess) return e;
   const unsigned grid = unsigned(std::min(tiles, size_t(cus)));
   hipLaunchKernelGGL(encode_k1024_fused, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
                      uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride),

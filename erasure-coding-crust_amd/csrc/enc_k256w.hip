@@ -463,7 +463,7 @@ hipError_t launch_encode_k256w(const CodeParams &p, const DevTables &t, const ui
   if (!scratch || tiles >= (size_t(1) << 32) - size_t(4) * cus) return hipErrorInvalidValue;
   // the tile counter (k256w_scratch_bytes), zeroed in stream order
   uint32_t *tick = static_cast<uint32_t *>(scratch);
-  if (const hipError_t e = hipMemsetAsync(tick, 0, sizeof(uint32_t), s); e != hipSuccess) return e;
+  if (const hipError_t e = launch_zero_counters(tick, sizeof(uint32_t), s); e != hipSuccess) return e;
   const size_t slots = 2 * size_t(cus);  // two workgroups per CU
   const unsigned grid = unsigned(tiles < slots ? tiles : slots);
   hipLaunchKernelGGL(encode_k256w, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads, uint64_t(plen),

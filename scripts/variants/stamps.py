@@ -110,34 +110,23 @@ elif kind == "enc4":
             "  Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);  // index 0 (the IFFT)\n  __syncthreads();\n" + STAMP)
     s = rep(s, "    // systematic shards 0..1023 = the data symbols (poly_encoder.hpp:239)\n",
             "    STAMP(0);\n    // systematic shards 0..1023 = the data symbols (poly_encoder.hpp:239)\n")
-    s = rep(s, "    // the index-0 tables (the last tile's DMA, issued before the 16 fast-form\n",
-            "    STAMP(1);\n    // the index-0 tables (the last tile's DMA, issued before the 16 fast-form\n")
-    s = rep(s, "    lds_barrier();\n    if (!idle) {\n      to_tower(g0, g1);",
-            "    lds_barrier();\n    STAMP(2);\n    if (!idle) {\n      to_tower(g0, g1);")
-    s = rep(s, "    lds_barrier();  // every wave is done with the index-0 tables\n",
-            "    STAMP(3);\n    lds_barrier();  // every wave is done with the index-0 tables\n")
+    s = rep(s, "    // the index-0 tables (the last tile's DMA, issued before the systematic\n",
+            "    STAMP(1);\n    // the index-0 tables (the last tile's DMA, issued before the systematic\n")
+    s = rep(s, "    lds_barrier();\n    if (!idle) {\n      to_tower(g);",
+            "    lds_barrier();\n    STAMP(2);\n    if (!idle) {\n      to_tower(g);")
+    s = rep(s, "    if (tid0 == 0) *slot = taken;  // (issued at the tile start: long returned)\n",
+            "    STAMP(3);\n    if (tid0 == 0) *slot = taken;  // (issued at the tile start: long returned)\n")
     s = rep(s, "      constexpr uint32_t s = decltype(cs)::value;\n",
             "      constexpr uint32_t s = decltype(cs)::value;\n      STAMP(4);\n")
-    s = rep(s, "      lds_barrier();  // (all waves' slices) and the regions are free\n",
-            "      lds_barrier();  // (all waves' slices) and the regions are free\n      STAMP(2);\n")
-    s = rep(s, "        to_tower(g0, g1);  // back to symbol coordinates\n      }\n",
-            "        to_tower(g0, g1);  // back to symbol coordinates\n      }\n      STAMP(5);\n")
-    s = rep(s, """        if (hf) lds_barrier();
-        if (!idle) stage_half(g0, g1, my, lane, wave, hf);
-        lds_barrier();
-        if (hf == 0)""", """        if (hf) lds_barrier();
-        STAMP(7);
-        if (!idle) stage_half(g0, g1, my, lane, wave, hf);
-        STAMP(8);
-        lds_barrier();
-        STAMP(7);
-        if (hf == 0)""")
-    s = rep(s, "        store_half(regions, SH, sstride, s * K + 512 * hf, nv, piece0, npieces, wave, lane);\n      }\n    };",
-            "        STAMP(9);\n        store_half(regions, SH, sstride, s * K + 512 * hf, nv, piece0, npieces, wave, lane);\n        STAMP(10);\n      }\n    };")
-    s = rep(s, "    if (ncos > 3) coset(std::integral_constant<uint32_t, 3>());\n  }\n",
-            "    if (ncos > 3) coset(std::integral_constant<uint32_t, 3>());\n    STAMP(1);\n  }\n" + FLUSH)
-    names = ["load", "sys+stage+stores", "vmcnt+barrier", "ifft", "coef+barrier", "fft", "-", "barriers", "stage",
-             "dma+coef", "stores"]
+    s = rep(s, "      lds_barrier();\n      if (!idle) {\n        if constexpr (s > 1) {",
+            "      lds_barrier();\n      STAMP(2);\n      if (!idle) {\n        if constexpr (s > 1) {")
+    s = rep(s, "        stage_rows(g, my, lane);\n      }\n      lds_barrier();",
+            "        stage_rows(g, my, lane);\n      }\n      STAMP(5);\n      lds_barrier();")
+    s = rep(s, "      store_rows(regions, SH, sstride, s * K, nv, piece0, npieces, wave, lane);\n    };",
+            "      STAMP(6);\n      store_rows(regions, SH, sstride, s * K, nv, piece0, npieces, wave, lane);\n      STAMP(7);\n    };")
+    s = rep(s, "    cur = next;\n  }\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // no LDS-DMA outlives the workgroup\n",
+            "    STAMP(1);\n    cur = next;\n  }\n" + FLUSH + "  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // no LDS-DMA outlives the workgroup\n")
+    names = ["load", "sys+stage+stores", "vmcnt+barrier", "ifft", "coset start", "fft+stage", "barrier+dma", "stores"]
 elif kind == "dec4":
     s = open(f"{ROOT}/erasure-coding-crust_amd/csrc/dec_n4096.hip").read()
     s = rep(s, "namespace ecamd {\nnamespace {", "namespace ecamd {\n__device__ unsigned long long g_stamp[16];\nnamespace {")
@@ -153,9 +142,9 @@ elif kind == "dec4":
             "        asm volatile(\"\" : \"+v\"(P.l[r]), \"+v\"(P.h[r]), \"+v\"(Qa.l[r]), \"+v\"(Qa.h[r]));\n      __builtin_amdgcn_sched_barrier(0);\n      STAMP(4);\n    };")
     s = rep(s, "    lds_barrier();  // every wave is done with the FFT tables\n",
             "    STAMP(5);\n    lds_barrier();  // every wave is done with the FFT tables\n")
-    s = rep(s, "    lds_barrier();\n    if (idle) continue;\n", "    lds_barrier();\n    STAMP(6);\n    if (idle) continue;\n")
-    s = rep(s, "        reinterpret_cast<uint4 *>(dst)[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);\n      }\n    }\n  }\n}",
-            "        reinterpret_cast<uint4 *>(dst)[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);\n      }\n    }\n    STAMP(7);\n  }\n" + FLUSH + "}")
+    s = rep(s, "    lds_barrier();\n    if (idle) {\n", "    lds_barrier();\n    STAMP(6);\n    if (idle) {\n")
+    s = rep(s, "        reinterpret_cast<uint4 *>(dst)[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);\n      }\n    }\n    tile = nxt;\n  }\n}",
+            "        reinterpret_cast<uint4 *>(dst)[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);\n      }\n    }\n    STAMP(7);\n    tile = nxt;\n  }\n" + FLUSH + "}")
     names = ["gather", "wait_tab+bar", "ifft", "bar+dma", "accum", "deriv+fft", "outtab", "output"]
 else:
     sys.exit("kind: enc | dec | encw | decw | enc4 | dec4")
