@@ -84,10 +84,11 @@ bool encode_host(const CodeParams &p, const uint8_t *payload, size_t len, HostCt
     ScratchLease lease(d, encode_scratch_bytes(p, len, 1), c->stream);
     if (!lease.ok()) return false;
     std::memcpy(c->h_in, payload, len);
+    HostSig sig = call_signal(c);  // stored by the encode kernel itself when it can (HostSig)
     if (!hip_check(launch_encode(p, device_tables(d), c->h_in, len, len, 1, c->h_out, dstride,
-                                 lease.ptr(), c->stream),
+                                 lease.ptr(), c->stream, &sig),
                    "encode launch") ||
-        !finish_call(c, "encode"))
+        !finish_call(c, "encode", &sig))
       return false;
     *sl_out = sl;
     return true;
@@ -136,9 +137,10 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
                                            hipMemcpyHostToDevice, c->stream),
                             "H2D"))
     return false;
+  HostSig sig = direct ? call_signal(c) : HostSig();
   if (all_systematic) {
     // every systematic shard is present: decode == interleave (exact)
-    if (!hip_check(launch_systematic(p, src, sl, dstride, 1, dst, out_bytes, c->stream),
+    if (!hip_check(launch_systematic(p, src, sl, dstride, 1, dst, out_bytes, c->stream, &sig),
                    "systematic launch"))
       return false;
   } else {
@@ -159,14 +161,15 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
     // path: the locator cache recycles entries nobody holds).  Kernels only
     // (direct): the signal-kernel wait; after a D2H copy the copy-to-kernel
     // hand-off makes that slower than waiting on the stream
-    const bool synced = direct ? finish_call(c, "reconstruct")
+    const bool synced = direct ? finish_call(c, "reconstruct", &sig)
                                : hip_check(hipStreamSynchronize(c->stream), "reconstruct");
     return launched && copied && synced;
   }
   return (direct || hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost,
                                              c->stream),
                               "D2H")) &&
-         (direct ? finish_call(c, "reconstruct") : hip_check(hipStreamSynchronize(c->stream), "reconstruct"));
+         (direct ? finish_call(c, "reconstruct", &sig)
+                 : hip_check(hipStreamSynchronize(c->stream), "reconstruct"));
 }
 
 bool take_output(HostCtx *c, size_t bytes, DataBlock *out) {

@@ -23,10 +23,42 @@ __device__ __forceinline__ void ld(uint2 *p, uint32_t &l, uint32_t &h) {
   h = v.y;
 }
 
-// inverse_afft (additive_fft.hpp:99-119) on S[pos * G + g], pos < 2^logsz
+// inverse_afft (additive_fft.hpp:99-119) on S[pos * G + g], pos < 2^logsz.
+// Small transforms (<= 3 stages, at most one butterfly per thread and stage:
+// the per-call sizes of tiny codes, e.g. n_validators 6) request every
+// stage's table up front, so the stages wait on one table latency instead of
+// one each (the per-call C ABI's kernel time).
+constexpr int kPreStages = 3;
 __device__ void ifft_g(uint2 *S, int logG, int logsz, uint32_t index, const DevTables t) {
   const int G = 1 << logG;
   const int half = (1 << logsz) >> 1;
+  if (logsz <= kPreStages && half * G <= int(blockDim.x)) {
+    const int b = threadIdx.x, g = b & (G - 1), pi = b >> logG;
+    const bool on = b < half * G;
+    Tab T[kPreStages];
+#pragma unroll
+    for (int m = 0; m < kPreStages; ++m) {
+      const int d = 1 << m, i = ((pi >> m) << (m + 1)) | (pi & (d - 1)), j = (i & ~(2 * d - 1)) | d;
+      if (on && m < logsz) load_tab(t.mslot, j - 1 + index, T[m]);
+    }
+#pragma unroll
+    for (int m = 0; m < kPreStages; ++m) {
+      if (m >= logsz) break;
+      const int d = 1 << m, i = ((pi >> m) << (m + 1)) | (pi & (d - 1));
+      if (on) {
+        uint32_t al, ah, bl, bh;
+        ld(S + i * G + g, al, ah);
+        ld(S + (i + d) * G + g, bl, bh);
+        bl ^= al;
+        bh ^= ah;
+        mul_acc(bl, bh, T[m], al, ah);
+        S[i * G + g] = make_uint2(al, ah);
+        S[(i + d) * G + g] = make_uint2(bl, bh);
+      }
+      __syncthreads();
+    }
+    return;
+  }
   for (int m = 0; m < logsz; ++m) {
     const int d = 1 << m;
     for (int b = threadIdx.x; b < half * G; b += blockDim.x) {
@@ -34,7 +66,7 @@ __device__ void ifft_g(uint2 *S, int logG, int logsz, uint32_t index, const DevT
       const int i = ((pi >> m) << (m + 1)) | (pi & (d - 1));
       const int j = (i & ~(2 * d - 1)) | d;
       Tab T;
-      load_tab(t.mtab, t.skews[j - 1 + index], T);
+      load_tab(t.mslot, j - 1 + index, T);  // (mtab[skews[..]]: no dependent load)
       uint32_t al, ah, bl, bh;
       ld(S + i * G + g, al, ah);
       ld(S + (i + d) * G + g, bl, bh);
@@ -48,10 +80,37 @@ __device__ void ifft_g(uint2 *S, int logG, int logsz, uint32_t index, const DevT
   }
 }
 
-// afft (additive_fft.hpp:121-141)
+// afft (additive_fft.hpp:121-141); small transforms as in ifft_g
 __device__ void fft_g(uint2 *S, int logG, int logsz, uint32_t index, const DevTables t) {
   const int G = 1 << logG;
   const int half = (1 << logsz) >> 1;
+  if (logsz <= kPreStages && half * G <= int(blockDim.x)) {
+    const int b = threadIdx.x, g = b & (G - 1), pi = b >> logG;
+    const bool on = b < half * G;
+    Tab T[kPreStages];
+#pragma unroll
+    for (int m = 0; m < kPreStages; ++m) {
+      const int d = 1 << m, i = ((pi >> m) << (m + 1)) | (pi & (d - 1)), j = (i & ~(2 * d - 1)) | d;
+      if (on && m < logsz) load_tab(t.mslot, j - 1 + index, T[m]);
+    }
+#pragma unroll
+    for (int m = kPreStages - 1; m >= 0; --m) {
+      if (m >= logsz) continue;
+      const int d = 1 << m, i = ((pi >> m) << (m + 1)) | (pi & (d - 1));
+      if (on) {
+        uint32_t al, ah, bl, bh;
+        ld(S + i * G + g, al, ah);
+        ld(S + (i + d) * G + g, bl, bh);
+        mul_acc(bl, bh, T[m], al, ah);
+        bl ^= al;
+        bh ^= ah;
+        S[i * G + g] = make_uint2(al, ah);
+        S[(i + d) * G + g] = make_uint2(bl, bh);
+      }
+      __syncthreads();
+    }
+    return;
+  }
   for (int m = logsz - 1; m >= 0; --m) {
     const int d = 1 << m;
     for (int b = threadIdx.x; b < half * G; b += blockDim.x) {
@@ -59,7 +118,7 @@ __device__ void fft_g(uint2 *S, int logG, int logsz, uint32_t index, const DevTa
       const int i = ((pi >> m) << (m + 1)) | (pi & (d - 1));
       const int j = (i & ~(2 * d - 1)) | d;
       Tab T;
-      load_tab(t.mtab, t.skews[j - 1 + index], T);
+      load_tab(t.mslot, j - 1 + index, T);
       uint32_t al, ah, bl, bh;
       ld(S + i * G + g, al, ah);
       ld(S + (i + d) * G + g, bl, bh);
@@ -71,6 +130,15 @@ __device__ void fft_g(uint2 *S, int logG, int logsz, uint32_t index, const DevTa
     }
     __syncthreads();
   }
+}
+
+// the fused completion signal (HostSig): every thread's output is made
+// visible at system scope, then one lane stores v
+__device__ __forceinline__ void signal_end(uint32_t *flag, uint32_t v) {
+  if (!flag) return;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // reed-solomon.hpp:47-81 + poly_encoder.hpp:31-86,217-240 for 4*G pieces
@@ -79,7 +147,7 @@ __global__ void __launch_bounds__(kBlock) encode_g(const uint8_t *__restrict__ p
                                                    uint8_t *__restrict__ shards, uint64_t slen,
                                                    uint64_t sstride, int nv, int logn, int logk,
                                                    int logG, uint32_t batch, DevTables t,
-                                                   uint2 *scratch) {
+                                                   uint2 *scratch, uint32_t *sig_flag, uint32_t sig_v) {
   extern __shared__ __attribute__((aligned(16))) uint2 smem[];
   const int k = 1 << logk, n = 1 << logn, G = 1 << logG;
   const uint64_t npieces = slen / 2;
@@ -138,6 +206,7 @@ __global__ void __launch_bounds__(kBlock) encode_g(const uint8_t *__restrict__ p
     __syncthreads();
   }
   }
+  signal_end(sig_flag, sig_v);  // (single-workgroup launches only)
 }
 
 // poly_encoder.hpp:90-116 in the folded n-point form: one
@@ -427,7 +496,8 @@ __global__ void __launch_bounds__(kBlock) reconstruct_g(
 __global__ void __launch_bounds__(kBlock) systematic_g(const uint8_t *__restrict__ shards,
                                                        uint64_t slen, uint64_t sstride, int nv,
                                                        int logk, uint8_t *__restrict__ out,
-                                                       uint64_t ostride, uint32_t batch) {
+                                                       uint64_t ostride, uint32_t batch,
+                                                       uint32_t *sig_flag, uint32_t sig_v) {
   const int k = 1 << logk;
   const uint64_t npos = slen / 2;
   const uint64_t total = npos * k;
@@ -442,6 +512,7 @@ __global__ void __launch_bounds__(kBlock) systematic_g(const uint8_t *__restrict
       O[2 * e + 1] = SH[uint64_t(y) * sstride + 2 * i + 1];
     }
   }
+  signal_end(sig_flag, sig_v);  // (single-workgroup launches only)
 }
 
 // completion signal of a per-call C-ABI call: after the call's work on the
@@ -496,7 +567,7 @@ size_t encode_scratch_bytes(const CodeParams &p, size_t plen, size_t batch) {
 
 hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                          size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
-                         size_t sstride, void *scratch, hipStream_t s) {
+                         size_t sstride, void *scratch, hipStream_t s, HostSig *sig) {
   if (batch == 0 || plen == 0) return hipSuccess;
   const bool aligned = (reinterpret_cast<uintptr_t>(d_payloads) % 16 == 0) &&
                        (reinterpret_cast<uintptr_t>(d_shards) % 8 == 0) &&
@@ -517,10 +588,13 @@ hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t 
   const bool lds = p.k <= uint32_t(kLdsSlots);
   const size_t shm = lds ? 2 * size_t(p.k) * G * sizeof(uint2) : 0;
   dim3 grid((unsigned)tiles, (unsigned)grid_y(batch));
+  const bool fuse = sig && sig->flag && grid.x * grid.y == 1;
+  if (fuse) sig->fused = true;
   hipLaunchKernelGGL(encode_g, grid, dim3(kBlock), shm, s, d_payloads, uint64_t(plen),
                      uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride), int(p.nv),
                      ilog2(p.n), ilog2(p.k), ilog2(uint32_t(G)), uint32_t(batch), t,
-                     lds ? nullptr : static_cast<uint2 *>(scratch));
+                     lds ? nullptr : static_cast<uint2 *>(scratch), fuse ? sig->flag : nullptr,
+                     fuse ? sig->v : 0u);
   return hipGetLastError();
 }
 
@@ -642,14 +716,16 @@ hipError_t launch_reconstruct(const CodeParams &p, const DevTables &t, const uin
 
 hipError_t launch_systematic(const CodeParams &p, const uint8_t *d_shards, size_t slen,
                              size_t sstride, size_t batch, uint8_t *d_out, size_t ostride,
-                             hipStream_t s) {
+                             hipStream_t s, HostSig *sig) {
   if (batch == 0 || slen < 2) return hipSuccess;
   const size_t total = slen / 2 * p.k;
   size_t blocks = (total + kBlock - 1) / kBlock;
   if (blocks > 4096) blocks = 4096;
+  const bool fuse = sig && sig->flag && blocks * grid_y(batch) == 1;
+  if (fuse) sig->fused = true;
   hipLaunchKernelGGL(systematic_g, dim3(unsigned(blocks), unsigned(grid_y(batch))), dim3(kBlock), 0,
                      s, d_shards, uint64_t(slen), uint64_t(sstride), int(p.nv), ilog2(p.k), d_out,
-                     uint64_t(ostride), uint32_t(batch));
+                     uint64_t(ostride), uint32_t(batch), fuse ? sig->flag : nullptr, fuse ? sig->v : 0u);
   return hipGetLastError();
 }
 

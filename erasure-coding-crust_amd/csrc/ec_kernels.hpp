@@ -63,6 +63,17 @@ struct DevTables {
   const uint8_t *timg_t = nullptr;     // kTabImages x kTabImageBytes, tower images
   const uint8_t *timg_f9 = nullptr;    // kF9Images x kTabImageBytes, F9 variants of tower image 0
   const uint8_t *cimg = nullptr;       // kCImgBytes, the element-indexed compact image
+  const MulTab *mslot = nullptr;       // 65535, mslot[i] = mtab[skews[i]]: by skew slot, one load
+};
+
+// Completion signal of a per-call C-ABI call fused into its last kernel: when
+// the launcher's kernel runs as a single workgroup it stores v to *flag at
+// system scope after its own output (fused = true); otherwise the caller
+// launches the separate signal kernel (finish_call).
+struct HostSig {
+  uint32_t *flag = nullptr;
+  uint32_t v = 0;
+  bool fused = false;
 };
 
 // Per (device, kernel), once and thread-safe: raise `fn`'s dynamic-LDS limit
@@ -79,7 +90,7 @@ size_t reconstruct_scratch_bytes(const CodeParams &p, size_t shard_len, size_t b
 
 hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                          size_t payload_len, size_t payload_stride, size_t batch, uint8_t *d_shards,
-                         size_t shard_stride, void *scratch, hipStream_t s);
+                         size_t shard_stride, void *scratch, hipStream_t s, HostSig *sig = nullptr);
 
 // Erasure locators (poly_encoder.hpp:90-116, folded form), one workgroup per
 // row of d_present.  d_pattern (nullable): rows b with d_pattern[b] != b are
@@ -114,7 +125,7 @@ hipError_t launch_reconstruct(const CodeParams &p, const DevTables &t, const uin
 
 hipError_t launch_systematic(const CodeParams &p, const uint8_t *d_shards, size_t shard_len,
                              size_t shard_stride, size_t batch, uint8_t *d_out, size_t out_stride,
-                             hipStream_t s);
+                             hipStream_t s, HostSig *sig = nullptr);
 
 // specialised kernels (enc_k256.hip)
 bool k256_applicable(const CodeParams &p);

@@ -23,6 +23,7 @@ struct DeviceState {
   uint8_t *timg_t = nullptr;
   uint8_t *timg_f9 = nullptr;
   uint8_t *cimg = nullptr;
+  MulTab *mslot = nullptr;  // mtab by skew slot (DevTables::mslot)
   std::mutex mu;
   std::map<uint32_t, uint16_t *> fold;
   std::mutex scratch_mu;  // held by a ScratchLease
@@ -71,6 +72,10 @@ const char *last_error() { return t_err.c_str(); }
 
 DeviceState *device_state() {
   int dev = -1, count = 0;
+  // this thread's last device, if still current: no device count, no lock
+  // (the per-call C ABI asks this two or three times per call)
+  thread_local DeviceState *t_last = nullptr;
+  if (t_last && hipGetDevice(&dev) == hipSuccess && dev == t_last->id) return t_last;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
     set_error("erasure_coding_crust(amd): no HIP device available (the HIP path is required; "
               "there is no CPU fallback)");
@@ -80,7 +85,7 @@ DeviceState *device_state() {
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_dev.size() < size_t(count)) g_dev.resize(count);
   auto &slot = g_dev[dev];
-  if (slot) return slot.get();
+  if (slot) return t_last = slot.get();
   const Field &f = field();
   auto st = std::make_unique<DeviceState>();
   st->id = dev;
@@ -160,6 +165,14 @@ DeviceState *device_state() {
       !hip_ok(hipMemcpy(st->timg_t, img_t.data(), img_t.size(), hipMemcpyHostToDevice),
               "upload tower images"))
     return nullptr;
+  {  // the multiply tables by skew slot (the generic kernels: one load per table)
+    std::vector<MulTab> ms(f.skews.size());
+    for (size_t i = 0; i < ms.size(); ++i) ms[i] = f.mtab[f.skews[i]];
+    if (!hip_ok(hipMalloc(&st->mslot, ms.size() * sizeof(MulTab)), "hipMalloc(mslot)") ||
+        !hip_ok(hipMemcpy(st->mslot, ms.data(), ms.size() * sizeof(MulTab), hipMemcpyHostToDevice),
+                "upload mslot"))
+      return nullptr;
+  }
   if (!hip_ok(hipMalloc(&st->mtab_t, 2 * f.mtab.size() * sizeof(MulTab)), "hipMalloc(tower mtab)") ||
       !hip_ok(hipMemcpy(st->mtab_t, f.mtab_tin.data(), f.mtab_tin.size() * sizeof(MulTab),
                         hipMemcpyHostToDevice),
@@ -177,7 +190,7 @@ DeviceState *device_state() {
     (void)hipFree(warm);
   }
   slot = std::move(st);
-  return slot.get();
+  return t_last = slot.get();
 }
 
 DevTables device_tables(DeviceState *d) {
@@ -190,6 +203,7 @@ DevTables device_tables(DeviceState *d) {
   t.timg_t = d->timg_t;
   t.timg_f9 = d->timg_f9;
   t.cimg = d->cimg;
+  t.mslot = d->mslot;
   return t;
 }
 
@@ -491,12 +505,12 @@ HostCtx::~HostCtx() {
   if (switched) (void)hipSetDevice(cur);
 }
 
-bool finish_call(HostCtx *c, const char *what) {
-  const auto sync = [&]() { return hip_ok(hipStreamSynchronize(c->stream), what); };
+HostSig call_signal(HostCtx *c) {
+  HostSig s;
   if (!c->h_flag) {
     if (hipHostMalloc(reinterpret_cast<void **>(&c->h_flag), 64, hipHostMallocDefault) != hipSuccess) {
       c->h_flag = nullptr;
-      return sync();
+      return s;
     }
     // a recycled pinned word may hold any stale value: start from a known one
     __atomic_store_n(c->h_flag, 0u, __ATOMIC_RELEASE);
@@ -504,7 +518,17 @@ bool finish_call(HostCtx *c, const char *what) {
   }
   uint32_t v = ++c->seq;
   if (v == 0) v = c->seq = 1;  // (wrap) 0 is the initial value
-  if (launch_signal_host(c->h_flag, v, c->stream) != hipSuccess) return sync();
+  s.flag = c->h_flag;
+  s.v = v;
+  return s;
+}
+
+bool finish_call(HostCtx *c, const char *what, const HostSig *sig) {
+  const auto sync = [&]() { return hip_ok(hipStreamSynchronize(c->stream), what); };
+  const HostSig s = sig ? *sig : call_signal(c);
+  if (!s.flag) return sync();
+  const uint32_t v = s.v;
+  if (!s.fused && launch_signal_host(s.flag, v, c->stream) != hipSuccess) return sync();
   // now and then ask the stream for an asynchronous error the spin cannot see
   const bool probe = (v & (kFinishProbeEvery - 1)) == 0;
   using clk = std::chrono::steady_clock;

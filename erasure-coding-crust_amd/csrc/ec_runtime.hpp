@@ -139,9 +139,16 @@ HostCtx *host_ctx();  // nullptr if no device
 // reports an asynchronous error).  False (error set) on a HIP error.
 // Every kFinishProbeEvery-th spin-completed call also queries the stream, so
 // an asynchronous kernel error is reported within that many calls.
+// sig: the completion word and sequence number of the call (call_signal),
+// offered to the call's last kernel launch first: if that kernel stored it
+// itself (HostSig::fused, a single-workgroup launch), no signal kernel is
+// launched.
 constexpr double kFinishSpinUs = 200.0;
 constexpr uint32_t kFinishProbeEvery = 16;
-bool finish_call(HostCtx *c, const char *what);
+bool finish_call(HostCtx *c, const char *what, const HostSig *sig = nullptr);
+// the next completion word / value of this context (flag null if the pinned
+// word could not be allocated: finish_call then synchronises the stream)
+HostSig call_signal(HostCtx *c);
 bool ensure_host(uint8_t **p, size_t *cap, size_t need);
 bool ensure_dev(void **p, size_t *cap, size_t need);
 
