@@ -1,0 +1,517 @@
+// dec_n1024x.hip — reconstruct for n = 1024, k = 256 (n_validators 766..1024,
+// the BASELINE headline) with 12 waves per CU: three per SIMD instead of the
+// two of reconstruct_n1024 (dec_n1024.hip), for the latency the 2-wave form
+// leaves exposed (31% of wave time waiting to issue, the
+// VALU ~57% busy at 2 waves per SIMD).
+//
+// The per-wave work is reconstruct_n1024's (one byte-planar group of 4 shard
+// columns per wave; gather + E[v] scaling, IFFT_1024 in radix-16 register
+// passes with wave-private LDS exchanges, the closed-form derivative and the
+// FFT restricted to the k outputs, phase 5: erased outputs times E[y]).  What
+// it takes to fit 12 waves in one CU:
+//  * LDS 160 KB = a 64 KB table image + 12 x 8 KB exchange regions.  The
+//    image (DevTables::dimg) holds planes 0 and 1 of every skew slot (the
+//    subfield tables of stages >= 2 need only those) and planes 2..4 only
+//    for the slots of IFFT stages 0 (general tables) and 1 (F9), compacted:
+//    stage-0 slot 2c -> entry c, stage-1 slot 4c + 1 -> entry 512 + c.
+//  * no staging of the received data rows in LDS: phase 5 reads its present
+//    rows y < k (8 B per lane and row) from the shards again (the gather
+//    has just read them: L2).
+//  * <= 168 VGPRs: the output tables E[y] are requested after IFFT pass C,
+//    not before the transform.
+// Tile = 48 shard columns (12 waves x 4); 1 MB at n_validators 1024 is 1954
+// columns, 41 tiles per payload.
+#include <hip/hip_runtime.h>
+
+#include "dec_n1024_common.hpp"
+#include "ec_device.hpp"
+#include "ec_kernels.hpp"
+
+namespace ecamd {
+namespace {
+using namespace n1024;
+constexpr int WAVES = 12;
+constexpr int THREADS = 64 * WAVES;
+constexpr int COLS = 4 * WAVES;  // shard columns per tile
+constexpr uint32_t PLANE = Tabs::kPlane;  // 16 KB: planes 0, 1 by skew slot
+constexpr uint32_t CP2 = 2 * PLANE, CP3 = CP2 + 768 * 16, CP4 = CP3 + 768 * 16;  // compact planes
+constexpr int TAB_REGION = int(CP4 + 512 * 16);
+static_assert(TAB_REGION == kDImgBytes, "the image layout (ec_kernels.hpp)");
+constexpr int LDS_BYTES = TAB_REGION + WAVES * REG_BYTES;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+constexpr int ROW_WORDS = COLS / 2;  // dwords of a row segment (96 B)
+
+// a general table of IFFT stage 0 / an F9 table of stage 1: planes 0, 1 at
+// the skew slot's address s, planes 2.. at the compact entry's address c
+__device__ __forceinline__ void tab_gen(uint32_t s, uint32_t c, Tab &T) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const auto rd = [](uint32_t a) { return *(const __attribute__((address_space(3))) v4u *)(uintptr_t(a)); };
+  const v4u p4 = rd(CP4 + c), p3 = rd(CP3 + c), p2 = rd(CP2 + c), p1 = rd(PLANE + s), p0 = rd(s);
+  const v4u p[5] = {p0, p1, p2, p3, p4};
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    T.t[4 * q] = p[q].x;
+    T.t[4 * q + 1] = p[q].y;
+    T.t[4 * q + 2] = p[q].z;
+    T.t[4 * q + 3] = p[q].w;
+  }
+}
+__device__ __forceinline__ void tab_f9(uint32_t s, uint32_t c, F9Tab &T) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const auto rd = [](uint32_t a) { return *(const __attribute__((address_space(3))) v4u *)(uintptr_t(a)); };
+  const v4u p3 = rd(CP3 + c), p2 = rd(CP2 + c), p1 = rd(PLANE + s), p0 = rd(s);
+  const v4u p[4] = {p0, p1, p2, p3};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    T.t[4 * q] = p[q].x;
+    T.t[4 * q + 1] = p[q].y;
+    T.t[4 * q + 2] = p[q].z;
+    T.t[4 * q + 3] = p[q].w;
+  }
+}
+
+// IFFT pass A (position bits 0-3 in registers, pos = 16 lane + r) on the
+// compact image: ipass4<0> with stage 0's general and stage 1's F9 tables
+// read as above (compact entry c = pos >> 1 at stage 0, 512 + (pos >> 2) at
+// stage 1; tlin is GF(2)-linear, so each address is a per-lane part XOR a
+// compile-time one)
+__device__ __forceinline__ void ipassA(S16 &s, uint32_t lane) {
+  const uint32_t ls = tlin(16 * lane), lc0 = tlin(8 * lane), lc1 = tlin(4 * lane) ^ tlin(512);
+  Tab T[2];
+  F9Tab F[2];
+  SubTab U[2];
+  const auto fetch = [&](int t, int blk, int slot) __attribute__((always_inline)) {
+    const uint32_t a = ls ^ tlin(skew_idx(uint32_t(blk), t));
+    if (t == 0) tab_gen(a, lc0 ^ tlin(uint32_t(blk) >> 1), T[slot]);
+    else if (t == 1) tab_f9(a, lc1 ^ tlin(uint32_t(blk) >> 2), F[slot]);
+    else tab_at(nullptr, a, U[slot]);
+  };
+  fetch(0, 0, 0);
+  int k = 0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int d = 1 << t;
+#pragma unroll
+    for (int blk = 0; blk < 16; blk += 2 * d, ++k) {
+      const int nt = blk + 2 * d < 16 ? t : t + 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
+      if (nt < 4) fetch(nt, nblk, (k + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < d; ++i) {
+        if (t >= 2) ib(s, blk + i, blk + i + d, U[k & 1]);
+        else if (t == 1) ib(s, blk + i, blk + i + d, F[k & 1]);
+        else ib(s, blk + i, blk + i + d, T[k & 1]);
+      }
+    }
+  }
+}
+
+// issue priority by transform phase (experiments): waves w, w + 4, w + 8
+// share a SIMD; N1024X_PRIO = 1 lets group 2 (w >= 8) lead pass A, group 1
+// pass B, group 0 pass C and the FFT; 2 the reverse; 0 equal throughout
+#ifndef N1024X_PRIO
+#define N1024X_PRIO 0
+#endif
+__device__ __forceinline__ void prio3(uint32_t wave_s, int phase) {
+  if constexpr (N1024X_PRIO != 0) {
+    const uint32_t lead = N1024X_PRIO == 1 ? 2u - uint32_t(phase) : uint32_t(phase);
+    if (phase < 3 && (wave_s >> 2) == lead) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(0);
+  }
+}
+
+// bytes [0, avail) (avail < 96) of a 16-B aligned row slice into w[24], zero
+// beyond: whole dwords at immediate offsets under a uniform count, the last
+// one masked (an aligned dword holding a wanted byte never crosses a page)
+__device__ __forceinline__ void load_row_tail96(const uint8_t *row, uint32_t avail, uint32_t (&w)[ROW_WORDS]) {
+  const uint32_t nw = (avail + 3) / 4;  // wave-uniform
+  const uint32_t last = (avail & 3) ? (1u << (8 * (avail & 3))) - 1 : ~0u;
+  const uint32_t *r = reinterpret_cast<const uint32_t *>(row);
+#pragma unroll
+  for (int j = 0; j < ROW_WORDS; ++j) {
+    w[j] = 0;
+    if (uint32_t(j) < nw) w[j] = r[j] & (uint32_t(j) + 1 == nw ? last : ~0u);
+  }
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
+    const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
+    const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
+    const uint32_t *__restrict__ pattern, const uint32_t *__restrict__ order,
+    uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t batch, DevTables t) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t *regions = lds + TAB_REGION;
+  const uint32_t tid0 = threadIdx.x, wave = tid0 >> 6;
+  uint8_t *my = regions + wave * REG_BYTES;
+
+  // the 64 KB image (DevTables::dimg), every load issued before the first store
+  {
+    constexpr int kPer = (TAB_REGION / 16 + THREADS - 1) / THREADS;
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = tid0 + k * THREADS;
+      if (i < uint32_t(TAB_REGION / 16)) v[k] = reinterpret_cast<const v4u *>(t.dimg)[i];
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = tid0 + k * THREADS;
+      if (i < uint32_t(TAB_REGION / 16)) reinterpret_cast<v4u *>(lds)[i] = v[k];
+    }
+  }
+  __syncthreads();
+
+  const uint64_t ncols = slen / 2;
+  const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);
+  const uint64_t total = uint64_t(tiles_pp) * batch;
+  const uint32_t wave_s = __builtin_amdgcn_readfirstlane(tid0 >> 6);
+  // m[0], m[1]: this thread's gather slots (gather_order: present rows first;
+  // slot tid and 768 + tid, the latter only below 1024): row << 16 |
+  // mul_index(E[row]), low half 0xFFFF = absent.  m[2], m[3]: the output rows
+  // y = 4 lane + q of phase 5, 16 bits each: 0xFFFF = present, else
+  // mul_index(E[y]).  Loaded one tile ahead.
+  TileWalk walk(blockIdx.x, gridDim.x, tiles_pp);
+  const auto load_meta = [&](uint64_t bw, uint32_t tid, uint32_t (&m)[4]) {
+    const uint64_t pt = pattern ? pattern[bw] : bw;
+    m[0] = order[bw * N + tid];
+    m[1] = tid + THREADS < uint32_t(N) ? order[bw * N + THREADS + tid] : 0xFFFFu;
+    const uint32_t y0 = 4 * (tid & 63);
+    const uint32_t p4 = *reinterpret_cast<const uint32_t *>(present + pt * N + y0);
+    const uint2 e4 = *reinterpret_cast<const uint2 *>(elog + pt * N + y0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t e = ((q < 2 ? e4.x : e4.y) >> (16 * (q & 1))) & 0xFFFFu;
+      const uint32_t f = ((p4 >> (8 * q)) & 0xFFu) ? 0xFFFFu : mul_index(e);
+      if (q & 1) m[2 + (q >> 1)] |= f << 16;
+      else m[2 + (q >> 1)] = f;
+    }
+  };
+  uint32_t meta[4] = {0, 0, 0, 0}, meta_next[4] = {0, 0, 0, 0};
+  if (blockIdx.x < total) load_meta(walk.b, tid0, meta);
+  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x, walk.advance()) {
+    // lane-derived addresses recomputed per tile (not hoisted and spilled)
+    uint32_t tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const uint32_t lane = tid & 63;
+    const uint64_t b = walk.b, col0 = walk.i * COLS;
+    const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
+    uint8_t *O = out + b * ostride;
+
+    // ---- phase 1: gather + scale this thread's slots' rows (decode_main:
+    // 174-177), 12 groups of 4 columns each into the groups' regions; absent
+    // rows as 0.  The first slot's row and E[v] table are requested before
+    // the tile barrier.
+    {
+      uint32_t w[ROW_WORDS] = {};  // (defined on every path: not carried across tiles)
+      Tab RT = {};
+      const uint64_t avail = slen - 2 * col0;  // bytes of a row inside the tile
+      const auto load_row = [&](int half) __attribute__((always_inline)) {
+        const uint8_t *row = SH + uint64_t(meta[half] >> 16) * sstride + 2 * col0;
+        if (avail >= 2 * COLS) {
+#pragma unroll
+          for (int q = 0; q < ROW_WORDS / 4; ++q) {
+            const uint4 d = reinterpret_cast<const uint4 *>(row)[q];
+            w[4 * q] = d.x;
+            w[4 * q + 1] = d.y;
+            w[4 * q + 2] = d.z;
+            w[4 * q + 3] = d.w;
+          }
+        } else {  // the payload's last tile
+          load_row_tail96(row, uint32_t(avail), w);
+        }
+        load_tab(t.mtab_tin, meta[half] & 0xffffu, RT);  // scaled into tower coordinates
+      };
+      if ((meta[0] & 0xffffu) != 0xffffu) load_row(0);
+      lds_barrier();  // the previous tile's readers of the regions are done
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        if (half == 1 && tid >= uint32_t(N - THREADS)) break;  // (uniform per wave)
+        const uint32_t v = meta[half] >> 16;
+        const bool on = (meta[half] & 0xffffu) != 0xffffu;
+        if (half == 1 && on) load_row(1);
+        uint32_t l[WAVES], h[WAVES];
+#pragma unroll
+        for (int g = 0; g < WAVES; ++g) l[g] = h[g] = 0;
+        if (on) {  // one divergent branch for the 12 groups
+#pragma unroll
+          for (int g = 0; g < WAVES; ++g) {  // columns 4g..4g+3: words (h0 l0 h1 l1)(h2 l2 h3 l3)
+            const uint32_t a = w[2 * g], c = w[2 * g + 1];
+            const uint32_t xh = vperm(c, a, 0x06040200u), xl = vperm(c, a, 0x07050301u);
+            mul_acc(xl, xh, RT, l[g], h[g]);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < WAVES; ++g)
+          *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l[g], h[g]);
+      }
+    }
+    if (tile + gridDim.x < total) {
+      uint64_t nb, ni;
+      walk.next_of(nb, ni);
+      load_meta(nb, tid, meta_next);
+    }
+    __syncthreads();
+    const uint64_t cbase = col0 + 4 * uint64_t(wave_s);  // wave-uniform
+    // a group past the payload's last column (the last, partial tile: 1 MB is
+    // 1954 columns, the 41st tile has 34): phases 2-5 are this wave's alone
+    if (cbase >= ncols) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) meta[i] = meta_next[i];
+      continue;
+    }
+
+    S16 s;
+    // ---- phase 2: IFFT_1024 on this wave's group
+    {  // layout A: v = 16*lane + r
+      const uint32_t la = lds_addr(my) | raddr(16 * lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint2 x = lds_ld2(la ^ raddr(r));
+        s.l[r] = x.x;
+        s.h[r] = x.y;
+      }
+      prio3(wave_s, 0);
+      ipassA(s, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) lds_st2(la ^ raddr(r), make_uint2(s.l[r], s.h[r]));
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    const uint32_t baseB = (lane & 15) | ((lane >> 4) << 8);  // layout B: bits 4-7 in registers
+    {
+      const uint32_t lb = lds_addr(my) | raddr(baseB);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint2 x = lds_ld2(lb ^ raddr(uint32_t(r) << 4));
+        s.l[r] = x.x;
+        s.h[r] = x.y;
+      }
+      prio3(wave_s, 1);
+      ipass4<4>(s, nullptr, tlin((lane >> 4) << 8));  // stages 4-7: subfield (planes 0, 1)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) lds_st2(lb ^ raddr(uint32_t(r) << 4), make_uint2(s.l[r], s.h[r]));
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    prio3(wave_s, 2);
+    // layout C: r bit0 = p8, bit1 = p9, bit2 = p6, bit3 = p7; lane = p0..p5
+    const uint32_t lc = lds_addr(my) | raddr(lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint2 x = lds_ld2(lc ^ raddr((uint32_t((r >> 2) & 3) << 6) | (uint32_t(r & 3) << 8)));
+      s.l[r] = x.x;
+      s.h[r] = x.y;
+    }
+    // IFFT stages 8 and 9 (index 0): stage 9 is b ^= a only, stage 8
+    // multiplies in its p9 = 1 block only (dec_n1024.hip)
+    {
+      SubTab Tb;
+      tab_at(nullptr, tlin(skew_idx(1u << 9, 8)), Tb);
+#pragma unroll
+      for (int hi = 0; hi < 4; ++hi) {
+        s.l[4 * hi + 1] ^= s.l[4 * hi];
+        s.h[4 * hi + 1] ^= s.h[4 * hi];
+      }
+#pragma unroll
+      for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi + 2, 4 * hi + 3, Tb);
+#pragma unroll
+      for (int hi = 0; hi < 4; ++hi) {
+        s.l[4 * hi + 2] ^= s.l[4 * hi];
+        s.h[4 * hi + 2] ^= s.h[4 * hi];
+      }
+    }
+
+    // phase-5 operands requested now, consumed after the derivative and the
+    // FFT: E[y] of this lane's erased output rows y = 4 lane + q, and the
+    // received ones (8 B of the row: this group's 4 columns)
+    Tab T5[4];
+    uint2 rv[4];
+    {
+      uint32_t ol2 = lane;
+      asm volatile("" : "+v"(ol2));
+      const bool whole = cbase + 4 <= ncols;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t m = (meta[2 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
+        rv[q] = make_uint2(0, 0);
+        // defined on every path (a table read only where used would be carried
+        // across the tile loop, and spilled, by the compiler)
+        load_tab(t.mtab_tout, m != 0xFFFFu ? m : 0u, T5[q]);  // tower in, symbols out
+        if (m == 0xFFFFu) {
+          const uint8_t *row = SH + uint64_t(4 * ol2 + q) * sstride + 2 * cbase;
+          rv[q] = whole ? *reinterpret_cast<const uint2 *>(row) : load8_any(row, uint32_t(2 * (ncols - cbase)));
+        }
+      }
+    }
+
+    // ---- phases 3 + 4: the closed-form derivative at y < 256 and the FFT
+    // restricted to y < 256 (dec_n1024.hip, the same steps)
+    uint32_t ql[4], qh[4];
+    {
+      const uint32_t keep0 = ((lane ^ (lane >> 1)) & 1) ? 0u : 0xffffffffu;
+      const uint32_t m4 = ((lane >> 4) & 1) ? 0u : 0xffffffffu;
+      const uint32_t m5 = ((lane >> 5) & 1) ? 0u : 0xffffffffu;
+      const auto lane_terms = [&](uint32_t c0, uint32_t acc) {
+        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(c0), 0xF5, 0xf, 0xf, false));  // quad [1,1,3,3]
+        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(c0), 0xEE, 0xf, 0xf, false));  // quad [2,3,2,3]
+        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(c0), 0x104, 0xf, 0x5, false));  // row_shl:4, banks 0, 2
+        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(c0), 0x108, 0xf, 0x3, false));  // row_shl:8, banks 0, 1
+        acc = __builtin_amdgcn_bitop3_b32(acc, from_upper(c0, 4), m4, 0x78);  // acc ^ (x & m)
+        acc = __builtin_amdgcn_bitop3_b32(acc, from_upper(c0, 5), m5, 0x78);
+        return __builtin_amdgcn_bitop3_b32(acc, c0, keep0, 0x78);
+      };
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t al = s.l[4 * q + 1] ^ s.l[4 * q + 2], ah = s.h[4 * q + 1] ^ s.h[4 * q + 2];
+        if (!(q & 1)) {  // p6 = 0
+          al ^= s.l[4 * (q | 1)];
+          ah ^= s.h[4 * (q | 1)];
+        }
+        if (!(q & 2)) {  // p7 = 0
+          al ^= s.l[4 * (q | 2)];
+          ah ^= s.h[4 * (q | 2)];
+        }
+        ql[q] = lane_terms(s.l[4 * q], al);
+        qh[q] = lane_terms(s.h[4 * q], ah);
+      }
+    }
+    {
+      auto fb = [&](int a, int bb, const SubTab &T) {  // every stage >= SUB for y < 256
+        mul_acc_sub(ql[bb], qh[bb], T, ql[a], qh[a]);
+        ql[bb] ^= ql[a];
+        qh[bb] ^= qh[a];
+      };
+      const uint32_t hi67 = ((lane >> 4) & 3) << 6, lo = lane & 15;
+      const uint32_t hi47 = ((lane >> 2) & 15) << 4, lo01 = lane & 3;
+      const uint32_t hi27 = lane << 2;
+      auto L = [&](int i) -> uint32_t {
+        switch (i) {
+          case 2: return tlin(skew_idx(1u << 7, 6));
+          case 3: return tlin(skew_idx(hi67 | lo, 5));
+          case 4: return tlin(skew_idx(hi67 | lo, 4));
+          case 5: return tlin(skew_idx(hi67 | 32u | lo, 4));
+          case 6: return tlin(skew_idx(hi47 | lo01, 3));
+          case 7: return tlin(skew_idx(hi47 | lo01, 2));
+          case 8: return tlin(skew_idx(hi47 | 8u | lo01, 2));
+          // stages 1, 0: the stage-2 slot of the same (subfield) skew element
+          case 9: return tlin(sub_alias(hi27, 1));
+          case 10: return tlin(sub_alias(hi27, 0));
+          default: return tlin(sub_alias(hi27 | 2u, 0));
+        }
+      };
+      const auto fx = [&](int a, int bb) {
+        ql[bb] ^= ql[a];
+        qh[bb] ^= qh[a];
+      };
+      SubTab T[2];
+      tab_at(nullptr, L(2), T[0]);
+      tab_at(nullptr, L(3), T[1]);
+      fx(0, 2);  // stage 7
+      fx(1, 3);
+      fx(0, 1);  // stage 6
+      fb(2, 3, T[0]);
+      tab_at(nullptr, L(4), T[0]);
+      swap_bit(ql[0], ql[1], 4, false);
+      swap_bit(qh[0], qh[1], 4, false);
+      swap_bit(ql[2], ql[3], 4, false);
+      swap_bit(qh[2], qh[3], 4, false);
+      swap_bit(ql[0], ql[2], 5, false);
+      swap_bit(qh[0], qh[2], 5, false);
+      swap_bit(ql[1], ql[3], 5, false);
+      swap_bit(qh[1], qh[3], 5, false);
+      fb(0, 2, T[1]);  // stage 5
+      fb(1, 3, T[1]);
+      tab_at(nullptr, L(5), T[1]);
+      fb(0, 1, T[0]);  // stage 4
+      tab_at(nullptr, L(6), T[0]);
+      fb(2, 3, T[1]);
+      tab_at(nullptr, L(7), T[1]);
+      const bool l2 = (lane >> 2) & 1, l3 = (lane >> 3) & 1;
+      swap_bit(ql[0], ql[1], 2, l2);
+      swap_bit(qh[0], qh[1], 2, l2);
+      swap_bit(ql[2], ql[3], 2, l2);
+      swap_bit(qh[2], qh[3], 2, l2);
+      swap_bit(ql[0], ql[2], 3, l3);
+      swap_bit(qh[0], qh[2], 3, l3);
+      swap_bit(ql[1], ql[3], 3, l3);
+      swap_bit(qh[1], qh[3], 3, l3);
+      fb(0, 2, T[0]);  // stage 3
+      fb(1, 3, T[0]);
+      tab_at(nullptr, L(8), T[0]);
+      fb(0, 1, T[1]);  // stage 2
+      tab_at(nullptr, L(9), T[1]);
+      fb(2, 3, T[0]);
+      tab_at(nullptr, L(10), T[0]);
+      const bool l0 = lane & 1, l1 = (lane >> 1) & 1;
+      swap_bit(ql[0], ql[1], 0, l0);
+      swap_bit(qh[0], qh[1], 0, l0);
+      swap_bit(ql[2], ql[3], 0, l0);
+      swap_bit(qh[2], qh[3], 0, l0);
+      swap_bit(ql[0], ql[2], 1, l1);
+      swap_bit(qh[0], qh[2], 1, l1);
+      swap_bit(ql[1], ql[3], 1, l1);
+      swap_bit(qh[1], qh[3], 1, l1);
+      fb(0, 2, T[1]);  // stage 1
+      fb(1, 3, T[1]);
+      tab_at(nullptr, L(11), T[1]);
+      fb(0, 1, T[0]);  // stage 0
+      fb(2, 3, T[1]);
+    }
+
+    prio3(wave_s, 3);
+    // ---- phase 5: y = 4*lane + q; columns cbase + c (decode_main:185-188,
+    // reconstructSub:138-149)
+    {
+      uint32_t ol[4], oh[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t m = (meta[2 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
+        ol[q] = oh[q] = 0;
+        if (m != 0xFFFFu) {
+          mul_acc(ql[q], qh[q], T5[q], ol[q], oh[q]);
+        } else {
+          oh[q] = vperm(rv[q].y, rv[q].x, 0x06040200u);
+          ol[q] = vperm(rv[q].y, rv[q].x, 0x07050301u);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint64_t col = cbase + c;
+        if (col >= ncols) break;
+        const uint32_t w0 = vperm(ol[0], oh[0], 0x0c0c0400u + 0x0101u * c) |
+                            (vperm(ol[1], oh[1], 0x0c0c0400u + 0x0101u * c) << 16);
+        const uint32_t w1 = vperm(ol[2], oh[2], 0x0c0c0400u + 0x0101u * c) |
+                            (vperm(ol[3], oh[3], 0x0c0c0400u + 0x0101u * c) << 16);
+        *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) meta[i] = meta_next[i];
+  }
+}
+
+hipError_t launch_reconstruct_n1024x(const CodeParams &p, const DevTables &t,
+                                     const uint8_t *d_shards, size_t slen, size_t sstride,
+                                     const uint8_t *d_present, const uint16_t *d_err_log,
+                                     const uint32_t *d_pattern, size_t batch, uint8_t *d_out,
+                                     size_t ostride, void *scratch, hipStream_t s) {
+  int cus = 0;
+  if (!t.dimg || !scratch || slen / 2 < size_t(COLS)) return hipErrorInvalidValue;
+  if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&reconstruct_n1024x), LDS_BYTES, &cus);
+      e != hipSuccess)
+    return e;
+  uint32_t *order = static_cast<uint32_t *>(scratch);  // gather_order_bytes(p, batch)
+  if (const hipError_t e = launch_gather_order(p, d_present, d_err_log, d_pattern, batch, order, s);
+      e != hipSuccess)
+    return e;
+  const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
+  const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
+  hipLaunchKernelGGL(reconstruct_n1024x, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards, uint64_t(slen),
+                     uint64_t(sstride), d_present, d_err_log, d_pattern, order, d_out, uint64_t(ostride),
+                     int(p.nv), uint32_t(batch), t);
+  return hipGetLastError();
+}
+
+}  // namespace ecamd

@@ -8,6 +8,8 @@
 // multiply is the v_perm lookup of ec_device.hpp.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "ec_device.hpp"
 #include "ec_kernels.hpp"
 
@@ -688,10 +690,18 @@ hipError_t launch_reconstruct(const CodeParams &p, const DevTables &t, const uin
   const bool out8 = reinterpret_cast<uintptr_t>(d_out) % 8 == 0 && (batch == 1 || ostride % 8 == 0) &&
                     reinterpret_cast<uintptr_t>(d_present) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(d_err_log) % 16 == 0;  // vector loads of flag / E rows
+  // ECCR_AMD_RECON_WAVES=8 (experiments): the 8-wave kernel where the 12-wave one applies
+  static const bool waves8 = [] {
+    const char *e = std::getenv("ECCR_AMD_RECON_WAVES");
+    return e && e[0] == '8';
+  }();
+  const bool packed1024 = n1024_packed(slen, reinterpret_cast<uintptr_t>(d_shards), sstride);
+  if (n1024_applicable(p) && !packed1024 && aligned && out8 && !waves8 && slen / 2 >= 48)
+    return launch_reconstruct_n1024x(p, t, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch,
+                                     d_out, ostride, scratch, s);
   if (n1024_applicable(p) &&
-      (n1024_packed(slen, reinterpret_cast<uintptr_t>(d_shards), sstride)
-           ? out8 && reinterpret_cast<uintptr_t>(d_shards) % 2 == 0 && sstride % 2 == 0
-           : aligned && out8))
+      (packed1024 ? out8 && reinterpret_cast<uintptr_t>(d_shards) % 2 == 0 && sstride % 2 == 0
+                  : aligned && out8))
     return launch_reconstruct_n1024(p, t, d_shards, slen, sstride, d_present, d_err_log, d_pattern, batch,
                                     d_out, ostride, scratch, s);
   if (aligned && n4096_applicable(p) && reinterpret_cast<uintptr_t>(d_out) % 16 == 0 &&

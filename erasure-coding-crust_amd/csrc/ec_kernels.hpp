@@ -54,6 +54,14 @@ __host__ __device__ constexpr uint32_t cimg_lin(uint32_t x) {
   return ((x >> 4) << 8) | (((x ^ (x >> 4) ^ (x >> 8)) & 15) << 4);
 }
 
+// Reduced F9 image 0 (reconstruct_n1024x, 12 waves per CU): planes 0 and 1 of
+// every slot as in the F9 image (kind 0) at 0 / 16384 (the subfield tables of
+// stages >= 2 use only those), planes 2, 3 of the stage-0 (general) and
+// stage-1 (F9) slots compacted at 32768 / 45056 (slot 2c -> entry c, slot
+// 4c + 1 -> entry 512 + c; entry e at tlin(e) = cimg_lin(e)) and plane 4 of
+// the stage-0 slots at 57344: 64 KB instead of 80.
+constexpr uint32_t kDImgBytes = 65536;
+
 struct DevTables {
   const uint16_t *skews = nullptr;     // 65535
   const MulTab *mtab = nullptr;        // 65536
@@ -64,6 +72,7 @@ struct DevTables {
   const uint8_t *timg_f9 = nullptr;    // kF9Images x kTabImageBytes, F9 variants of tower image 0
   const uint8_t *cimg = nullptr;       // kCImgBytes, the element-indexed compact image
   const MulTab *mslot = nullptr;       // 65535, mslot[i] = mtab[skews[i]]: by skew slot, one load
+  const uint8_t *dimg = nullptr;       // kDImgBytes, the reduced F9 image 0
 };
 
 // Completion signal of a per-call C-ABI call fused into its last kernel: when
@@ -176,6 +185,12 @@ hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
                                     const uint8_t *d_present, const uint16_t *d_err_log,
                                     const uint32_t *d_pattern, size_t batch, uint8_t *d_out,
                                     size_t ostride, void *scratch, hipStream_t s);
+// the 12-wave form (dec_n1024x.hip) for the unpacked case, same scratch
+hipError_t launch_reconstruct_n1024x(const CodeParams &p, const DevTables &t,
+                                     const uint8_t *d_shards, size_t slen, size_t sstride,
+                                     const uint8_t *d_present, const uint16_t *d_err_log,
+                                     const uint32_t *d_pattern, size_t batch, uint8_t *d_out,
+                                     size_t ostride, void *scratch, hipStream_t s);
 
 // specialised kernels (dec_n4096.hip); scratch: n4096_scratch_bytes(p, batch)
 bool n4096_applicable(const CodeParams &p);

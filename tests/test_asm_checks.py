@@ -59,3 +59,15 @@ def test_enc_k256w_fast_store_count(tmp_path):
     # own vmcnt(4) before the next tile's transposes depends on it too
     blocks = _nt_store_blocks(_asm("enc_k256w.hip", tmp_path), "encode_k256w")
     assert blocks and all(c == 4 for c in blocks), blocks
+
+
+def test_dec_n1024x_no_spills(tmp_path):
+    # dec_n1024x.hip runs 3 waves per SIMD only at <= 168 VGPRs (launch bounds
+    # 768); a loop-carried table or row array (a value read on a path that did
+    # not write it) pushes it into scratch spills, ~25% slower (round 5)
+    text = _asm("dec_n1024x.hip", tmp_path)
+    body = text[text.index("reconstruct_n1024x"):]
+    body = body[:body.index("s_endpgm")]
+    assert "scratch_" not in body
+    assert re.search(r"NumVgprs:\s+(\d+)", text), "resource summary missing"
+    assert all(int(v) <= 168 for v in re.findall(r"NumVgprs:\s+(\d+)", text))
