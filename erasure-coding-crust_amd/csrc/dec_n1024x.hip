@@ -40,6 +40,10 @@ static_assert(TAB_REGION == kDImgBytes, "the image layout (ec_kernels.hpp)");
 constexpr int LDS_BYTES = TAB_REGION + WAVES * REG_BYTES;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 constexpr int ROW_WORDS = COLS / 2;  // dwords of a row segment (96 B)
+// the tile schedule's LDS word: skew slot 1023 of plane 0, which no table
+// read touches (skew indices stop at 1022; sub_alias at 1019), free once the
+// image is copied
+constexpr uint32_t SLOT = tlin(1023);
 
 // a general table of IFFT stage 0 / an F9 table of stage 1: planes 0, 1 at
 // the skew slot's address s, planes 2.. at the compact entry's address c
@@ -70,39 +74,98 @@ __device__ __forceinline__ void tab_f9(uint32_t s, uint32_t c, F9Tab &T) {
   }
 }
 
-// IFFT pass A (position bits 0-3 in registers, pos = 16 lane + r) on the
-// compact image: ipass4<0> with stage 0's general and stage 1's F9 tables
-// read as above (compact entry c = pos >> 1 at stage 0, 512 + (pos >> 2) at
-// stage 1; tlin is GF(2)-linear, so each address is a per-lane part XOR a
-// compile-time one)
-__device__ __forceinline__ void ipassA(S16 &s, uint32_t lane) {
-  const uint32_t ls = tlin(16 * lane), lc0 = tlin(8 * lane), lc1 = tlin(4 * lane) ^ tlin(512);
-  Tab T[2];
-  F9Tab F[2];
-  SubTab U[2];
-  const auto fetch = [&](int t, int blk, int slot) __attribute__((always_inline)) {
-    const uint32_t a = ls ^ tlin(skew_idx(uint32_t(blk), t));
-    if (t == 0) tab_gen(a, lc0 ^ tlin(uint32_t(blk) >> 1), T[slot]);
-    else if (t == 1) tab_f9(a, lc1 ^ tlin(uint32_t(blk) >> 2), F[slot]);
-    else tab_at(nullptr, a, U[slot]);
-  };
-  fetch(0, 0, 0);
-  int k = 0;
+// A radix-16 inverse pass (position bits B0..B0+3 in registers) whose 15
+// tables run through a ring of R slots: table k is requested R - 1 tables
+// ahead of its use.  Table k: stage tk(k), block bk(k) (8 + 4 + 2 + 1).  A
+// slot holds a general table (20 words), an F9 table (16) or a subfield one
+// (5); only the words a table uses are live.  At stage 0 each table feeds one
+// butterfly (~90 issue cycles), so one table ahead leaves the LDS latency
+// under 12 waves exposed.
+constexpr int tk(int k) { return k < 8 ? 0 : k < 12 ? 1 : k < 14 ? 2 : 3; }
+constexpr int bk(int k) { return k < 8 ? 2 * k : k < 12 ? 4 * (k - 8) : k < 14 ? 8 * (k - 12) : 0; }
+
+#ifndef N1024X_RA
+#define N1024X_RA 2
+#endif
+#ifndef N1024X_RB
+#define N1024X_RB 3
+#endif
+
+// kind of a stage's table: 0 general, 1 F9, 2 subfield
+template <int B0, int T>
+constexpr int kind_of() { return B0 + T >= SUB ? 2 : (kF9 && B0 + T == 1) ? 1 : 0; }
+
+template <int KIND>
+__device__ __forceinline__ void ring_bfly(S16 &s, int a, int b, const Tab &R) {
+  if constexpr (KIND == 0) {
+    ib(s, a, b, R);
+  } else if constexpr (KIND == 1) {
+    F9Tab F;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int d = 1 << t;
+    for (int i = 0; i < 16; ++i) F.t[i] = R.t[i];
+    ib(s, a, b, F);
+  } else {
+    SubTab U;
 #pragma unroll
-    for (int blk = 0; blk < 16; blk += 2 * d, ++k) {
-      const int nt = blk + 2 * d < 16 ? t : t + 1, nblk = blk + 2 * d < 16 ? blk + 2 * d : 0;
-      if (nt < 4) fetch(nt, nblk, (k + 1) & 1);
+    for (int i = 0; i < 5; ++i) U.t[i] = R.t[i];
+    ib(s, a, b, U);
+  }
+}
+
+// fetch(k, slot): table k into `slot` (a Tab)
+template <int B0, int R, class Fetch>
+__device__ __forceinline__ void ipass_ring(S16 &s, Fetch &&fetch) {
+  Tab ring[R];
 #pragma unroll
-      for (int i = 0; i < d; ++i) {
-        if (t >= 2) ib(s, blk + i, blk + i + d, U[k & 1]);
-        else if (t == 1) ib(s, blk + i, blk + i + d, F[k & 1]);
-        else ib(s, blk + i, blk + i + d, T[k & 1]);
-      }
+  for (int k = 0; k < R - 1; ++k) fetch(k, ring[k]);
+#pragma unroll
+  for (int k = 0; k < 15; ++k) {
+    if (k + R - 1 < 15) fetch(k + R - 1, ring[(k + R - 1) % R]);
+    const int t = tk(k), blk = bk(k), d = 1 << t;
+#pragma unroll
+    for (int i = 0; i < d; ++i) {
+      if (t == 0) ring_bfly<kind_of<B0, 0>()>(s, blk + i, blk + i + d, ring[k % R]);
+      else if (t == 1) ring_bfly<kind_of<B0, 1>()>(s, blk + i, blk + i + d, ring[k % R]);
+      else if (t == 2) ring_bfly<kind_of<B0, 2>()>(s, blk + i, blk + i + d, ring[k % R]);
+      else ring_bfly<kind_of<B0, 3>()>(s, blk + i, blk + i + d, ring[k % R]);
     }
   }
+}
+
+// IFFT pass A (position bits 0-3 in registers, pos = 16 lane + r) on the
+// reduced image: stage 0's general and stage 1's F9 tables read as above
+// (compact entry c = pos >> 1 at stage 0, 512 + (pos >> 2) at stage 1; tlin
+// is GF(2)-linear, so each address is a per-lane part XOR a compile-time one)
+__device__ __forceinline__ void ipassA(S16 &s, uint32_t lane) {
+  const uint32_t ls = tlin(16 * lane), lc0 = tlin(8 * lane), lc1 = tlin(4 * lane) ^ tlin(512);
+  ipass_ring<0, N1024X_RA>(s, [&](int k, Tab &T) __attribute__((always_inline)) {
+    const int t = tk(k), blk = bk(k);
+    const uint32_t a = ls ^ tlin(skew_idx(uint32_t(blk), t));
+    if (t == 0) {
+      tab_gen(a, lc0 ^ tlin(uint32_t(blk) >> 1), T);
+    } else if (t == 1) {
+      F9Tab F;
+      tab_f9(a, lc1 ^ tlin(uint32_t(blk) >> 2), F);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) T.t[i] = F.t[i];
+    } else {
+      SubTab U;
+      tab_at(nullptr, a, U);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) T.t[i] = U.t[i];
+    }
+  });
+}
+
+// IFFT pass B (position bits 4-7 in registers): subfield tables only
+__device__ __forceinline__ void ipassB(S16 &s, uint32_t lane) {
+  const uint32_t lb = tlin((lane >> 4) << 8);
+  ipass_ring<4, N1024X_RB>(s, [&](int k, Tab &T) __attribute__((always_inline)) {
+    SubTab U;
+    tab_at(nullptr, lb ^ tlin(skew_idx(uint32_t(bk(k)) << 4, 4 + tk(k))), U);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) T.t[i] = U.t[i];
+  });
 }
 
 // issue priority by transform phase (experiments): waves w, w + 4, w + 8
@@ -139,10 +202,19 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
     const uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride,
     const uint8_t *__restrict__ present, const uint16_t *__restrict__ elog,
     const uint32_t *__restrict__ pattern, const uint32_t *__restrict__ order,
-    uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t batch, DevTables t) {
+    uint8_t *__restrict__ out, uint64_t ostride, int nv, uint32_t batch, uint32_t *tick, DevTables t) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *regions = lds + TAB_REGION;
+  // Tiles are handed out dynamically: a workgroup's first tile is blockIdx.x,
+  // every later one gridDim.x + a ticket from the counter *tick (zeroed by
+  // the launcher).  The ticket for the tile after next is taken by thread 0
+  // during a tile and published in the LDS word SLOT at its end (one tile of
+  // notice: the next tile's metadata is loaded a tile ahead).  A static
+  // grid stride left the workgroups' end times ~3.5% of the launch apart.
+  volatile uint32_t *slot = reinterpret_cast<volatile uint32_t *>(lds + SLOT);
   const uint32_t tid0 = threadIdx.x, wave = tid0 >> 6;
+  uint32_t taken = 0;
+  if (tid0 == 0) taken = gridDim.x + atomicAdd(tick, 1u);
   uint8_t *my = regions + wave * REG_BYTES;
 
   // the 64 KB image (DevTables::dimg), every load issued before the first store
@@ -162,6 +234,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
     }
   }
   __syncthreads();
+  if (tid0 == 0) *slot = taken;  // read after the first tile's region barrier
 
   const uint64_t ncols = slen / 2;
   const uint32_t tiles_pp = uint32_t((ncols + COLS - 1) / COLS);
@@ -172,7 +245,6 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
   // mul_index(E[row]), low half 0xFFFF = absent.  m[2], m[3]: the output rows
   // y = 4 lane + q of phase 5, 16 bits each: 0xFFFF = present, else
   // mul_index(E[y]).  Loaded one tile ahead.
-  TileWalk walk(blockIdx.x, gridDim.x, tiles_pp);
   const auto load_meta = [&](uint64_t bw, uint32_t tid, uint32_t (&m)[4]) {
     const uint64_t pt = pattern ? pattern[bw] : bw;
     m[0] = order[bw * N + tid];
@@ -189,16 +261,19 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
     }
   };
   uint32_t meta[4] = {0, 0, 0, 0}, meta_next[4] = {0, 0, 0, 0};
-  if (blockIdx.x < total) load_meta(walk.b, tid0, meta);
-  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x, walk.advance()) {
+  uint32_t cur = blockIdx.x;  // (total < 2^32: launcher)
+  if (cur < total) load_meta(cur / tiles_pp, tid0, meta);
+  while (cur < total) {
     // lane-derived addresses recomputed per tile (not hoisted and spilled)
     uint32_t tid = tid0;
     asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63;
-    const uint64_t b = walk.b, col0 = walk.i * COLS;
+    const uint32_t bq = cur / tiles_pp;
+    const uint64_t b = bq, col0 = uint64_t(cur - bq * tiles_pp) * COLS;
     const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
     uint8_t *O = out + b * ostride;
 
+    uint32_t nxt;  // the next tile (SLOT)
     // ---- phase 1: gather + scale this thread's slots' rows (decode_main:
     // 174-177), 12 groups of 4 columns each into the groups' regions; absent
     // rows as 0.  The first slot's row and E[v] table are requested before
@@ -225,6 +300,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
       };
       if ((meta[0] & 0xffffu) != 0xffffu) load_row(0);
       lds_barrier();  // the previous tile's readers of the regions are done
+      nxt = __builtin_amdgcn_readfirstlane(*slot);
+      if (tid0 == 0) taken = gridDim.x + atomicAdd(tick, 1u);  // the tile after nxt
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         if (half == 1 && tid >= uint32_t(N - THREADS)) break;  // (uniform per wave)
@@ -247,18 +324,15 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
           *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l[g], h[g]);
       }
     }
-    if (tile + gridDim.x < total) {
-      uint64_t nb, ni;
-      walk.next_of(nb, ni);
-      load_meta(nb, tid, meta_next);
-    }
-    __syncthreads();
+    if (nxt < total) load_meta(nxt / tiles_pp, tid, meta_next);
+    __syncthreads();  // (every wave has read SLOT)
     const uint64_t cbase = col0 + 4 * uint64_t(wave_s);  // wave-uniform
     // a group past the payload's last column (the last, partial tile: 1 MB is
     // 1954 columns, the 41st tile has 34): phases 2-5 are this wave's alone
     if (cbase >= ncols) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) meta[i] = meta_next[i];
+      cur = nxt;
       continue;
     }
 
@@ -289,7 +363,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
         s.h[r] = x.y;
       }
       prio3(wave_s, 1);
-      ipass4<4>(s, nullptr, tlin((lane >> 4) << 8));  // stages 4-7: subfield (planes 0, 1)
+      ipassB(s, lane);  // stages 4-7: subfield (planes 0, 1)
 #pragma unroll
       for (int r = 0; r < 16; ++r) lds_st2(lb ^ raddr(uint32_t(r) << 4), make_uint2(s.l[r], s.h[r]));
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -487,10 +561,19 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
         *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);
       }
     }
+    // thread 0 (wave 0 never idles: its columns start the tile) publishes the
+    // tile after next; the atomic returned during the transform
+    if (tid0 == 0) *slot = taken;
 #pragma unroll
     for (int i = 0; i < 4; ++i) meta[i] = meta_next[i];
+    cur = nxt;
   }
 }
+
+// scratch of the n = 1024 reconstructs: the gather order, then the tile
+// counter of reconstruct_n1024x (256 B apart)
+size_t n1024_tick_offset(const CodeParams &p, size_t batch) { return (gather_order_bytes(p, batch) + 255) / 256 * 256; }
+size_t n1024_scratch_bytes(const CodeParams &p, size_t batch) { return n1024_tick_offset(p, batch) + 256; }
 
 hipError_t launch_reconstruct_n1024x(const CodeParams &p, const DevTables &t,
                                      const uint8_t *d_shards, size_t slen, size_t sstride,
@@ -502,15 +585,18 @@ hipError_t launch_reconstruct_n1024x(const CodeParams &p, const DevTables &t,
   if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&reconstruct_n1024x), LDS_BYTES, &cus);
       e != hipSuccess)
     return e;
-  uint32_t *order = static_cast<uint32_t *>(scratch);  // gather_order_bytes(p, batch)
+  const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
+  if (tiles + 4096 >= (size_t(1) << 32)) return hipErrorInvalidValue;  // 32-bit tile tickets
+  uint32_t *order = static_cast<uint32_t *>(scratch);  // n1024_scratch_bytes(p, batch)
+  uint32_t *tick = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + n1024_tick_offset(p, batch));
   if (const hipError_t e = launch_gather_order(p, d_present, d_err_log, d_pattern, batch, order, s);
       e != hipSuccess)
     return e;
-  const size_t tiles = (slen / 2 + COLS - 1) / COLS * batch;
+  if (const hipError_t e = launch_zero_counters(tick, sizeof(uint32_t), s); e != hipSuccess) return e;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
   hipLaunchKernelGGL(reconstruct_n1024x, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_shards, uint64_t(slen),
                      uint64_t(sstride), d_present, d_err_log, d_pattern, order, d_out, uint64_t(ostride),
-                     int(p.nv), uint32_t(batch), t);
+                     int(p.nv), uint32_t(batch), tick, t);
   return hipGetLastError();
 }
 

@@ -672,8 +672,8 @@ hipError_t launch_broadcast_locators(const CodeParams &p, const uint32_t *d_patt
 
 size_t reconstruct_scratch_bytes(const CodeParams &p, size_t slen, size_t batch) {
   if (n4096_applicable(p)) return n4096_scratch_bytes(p, batch);
-  if (n1024_applicable(p) || decgen_applicable(p))
-    return gather_order_bytes(p, batch);
+  if (n1024_applicable(p)) return n1024_scratch_bytes(p, batch);
+  if (decgen_applicable(p)) return gather_order_bytes(p, batch);
   if (p.n <= uint32_t(kLdsSlots)) return 0;
   const size_t tiles = (slen / 2 + 3) / 4;
   return tiles * grid_y(batch) * 2 * size_t(p.n) * sizeof(uint2);

@@ -178,14 +178,17 @@ hipError_t launch_gather_order(const CodeParams &p, const uint8_t *d_present,
                                const uint16_t *d_err_log, const uint32_t *d_pattern, size_t batch,
                                uint32_t *order, hipStream_t s);
 
-// specialised kernels (dec_n1024.hip); scratch: gather_order_bytes(p, batch)
+// specialised kernels (dec_n1024.hip); scratch: n1024_scratch_bytes(p, batch)
 bool n1024_applicable(const CodeParams &p);
 hipError_t launch_reconstruct_n1024(const CodeParams &p, const DevTables &t,
                                     const uint8_t *d_shards, size_t slen, size_t sstride,
                                     const uint8_t *d_present, const uint16_t *d_err_log,
                                     const uint32_t *d_pattern, size_t batch, uint8_t *d_out,
                                     size_t ostride, void *scratch, hipStream_t s);
-// the 12-wave form (dec_n1024x.hip) for the unpacked case, same scratch
+// the 12-wave form (dec_n1024x.hip) for the unpacked case; both take
+// n1024_scratch_bytes (the gather order + the 12-wave form's tile counter)
+size_t n1024_scratch_bytes(const CodeParams &p, size_t batch);
+size_t n1024_tick_offset(const CodeParams &p, size_t batch);
 hipError_t launch_reconstruct_n1024x(const CodeParams &p, const DevTables &t,
                                      const uint8_t *d_shards, size_t slen, size_t sstride,
                                      const uint8_t *d_present, const uint16_t *d_err_log,

@@ -13,9 +13,14 @@ fi
 L=erasure-coding-crust_amd/lib
 for rep in $(seq 1 ${REPS:-2}); do
 for v in ${VARS:-main}; do
-  unset ECCR_AMD_RECON_WAVES
-  # w8: the default library with the 8-wave n = 1024 reconstruct
-  if [ $v = main ]; then unset ECC_AMD_LIB; elif [ $v = w8 ]; then unset ECC_AMD_LIB; export ECCR_AMD_RECON_WAVES=8; else export ECC_AMD_LIB=$PWD/$L/$v.so; fi
+  unset ECCR_AMD_RECON_WAVES ECCR_AMD_RECON_PACKED
+  # w8: the default library with the 8-wave n = 1024 reconstruct; w8p: its packed form
+  case $v in
+    main) unset ECC_AMD_LIB ;;
+    w8) unset ECC_AMD_LIB; export ECCR_AMD_RECON_WAVES=8 ;;
+    w8p) unset ECC_AMD_LIB; export ECCR_AMD_RECON_WAVES=8 ECCR_AMD_RECON_PACKED=1 ;;
+    *) export ECC_AMD_LIB=$PWD/$L/$v.so ;;
+  esac
   timeout -k 10 300 python bench.py --batch ${B:-4096} --steps ${STEPS:-5} --warmup 2 --sweep none --no-cpu-baseline ${ARGS:-} > $O/$v.json 2> $O/$v.err
   rc=$?
   if [ $rc -ne 0 ] && ! { [ $rc -eq 1 ] && [ "${v#diag}" != "$v" ]; }; then tail -5 $O/$v.err; exit 1; fi

@@ -17,6 +17,8 @@ that work costs in the real interleaving:
     dnobar  reconstruct_n1024: the two per-tile workgroup barriers dropped
     dnogat  reconstruct_n1024: the gather's row loads and E[v] multiplies dropped
     dnoout  reconstruct_n1024: the output stores dropped (values asm-consumed)
+    xnobar, xnogat, xnoout  the same three for reconstruct_n1024x (writes
+            OUTDIR/dec_n1024x.hip)
     kclk:F  the clk probe in the kernel of csrc file F (its first kernel with
             dynamic LDS), e.g. kclk:enc_k1024.hip (writes OUTDIR/F)
     dclk    the clk probe in reconstruct_n1024 instead (writes OUTDIR/dec_n1024.hip;
@@ -36,6 +38,7 @@ os.makedirs(out, exist_ok=True)
 enc = open(f"{CS}/enc_k256w.hip").read()
 cim = open(f"{CS}/cimg.hpp").read()
 dec = open(f"{CS}/dec_n1024.hip").read()
+decx = open(f"{CS}/dec_n1024x.hip").read()
 
 
 READER = '''
@@ -103,6 +106,19 @@ for k in kinds:
     elif k == "dnoout":
         dec = rep(dec, "        *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);\n",
                   "        asm volatile(\"\" :: \"v\"(w0), \"v\"(w1), \"v\"(O + (col * K + 4 * lane) * 2));\n")
+    elif k == "xnobar":
+        decx = rep(decx, "      lds_barrier();  // the previous tile's readers of the regions are done\n", "")
+        decx = rep(decx, "    __syncthreads();\n    const uint64_t cbase", "    const uint64_t cbase")
+        extra["dec_n1024x.hip"] = decx
+    elif k == "xnogat":
+        decx = rep(decx, "      if ((meta[0] & 0xffffu) != 0xffffu) load_row(0);\n", "")
+        decx = rep(decx, "        if (half == 1 && on) load_row(1);\n", "")
+        decx = rep(decx, "        if (on) {  // one divergent branch", "        if (meta[half] == 0x12345678u) {  //")
+        extra["dec_n1024x.hip"] = decx
+    elif k == "xnoout":
+        decx = rep(decx, "        *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);\n",
+                   "        asm volatile(\"\" :: \"v\"(w0), \"v\"(w1), \"v\"(O + (col * K + 4 * lane) * 2));\n")
+        extra["dec_n1024x.hip"] = decx
     elif k.startswith("kclk:"):
         fname = k.split(":", 1)[1]
         src = open(f"{CS}/{fname}").read()
