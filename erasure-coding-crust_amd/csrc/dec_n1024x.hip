@@ -84,6 +84,9 @@ __device__ __forceinline__ void tab_f9(uint32_t s, uint32_t c, F9Tab &T) {
 constexpr int tk(int k) { return k < 8 ? 0 : k < 12 ? 1 : k < 14 ? 2 : 3; }
 constexpr int bk(int k) { return k < 8 ? 2 * k : k < 12 ? 4 * (k - 8) : k < 14 ? 8 * (k - 12) : 0; }
 
+#ifndef N1024X_RV_EARLY
+#define N1024X_RV_EARLY 1
+#endif
 #ifndef N1024X_RA
 #define N1024X_RA 2
 #endif
@@ -336,6 +339,28 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
       continue;
     }
 
+    // phase 5's received rows y = 4 lane + q < 256 (8 B of the row: this
+    // group's 4 columns), re-read from the shards (L2: the gather has just
+    // read them; no LDS left to stage them), requested before the IFFT
+    // (N1024X_RV_EARLY = 0: after it; A/B at B = 4096: 10.68 / 10.92 ms
+    // against 10.76 / 11.00, and 154 VGPRs instead of 168)
+    uint2 rv[4];
+    const auto load_rv = [&]() __attribute__((always_inline)) {
+      uint32_t ol2 = lane;
+      asm volatile("" : "+v"(ol2));
+      const bool whole = cbase + 4 <= ncols;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t m = (meta[2 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
+        rv[q] = make_uint2(0, 0);
+        if (m == 0xFFFFu) {
+          const uint8_t *row = SH + uint64_t(4 * ol2 + q) * sstride + 2 * cbase;
+          rv[q] = whole ? *reinterpret_cast<const uint2 *>(row) : load8_any(row, uint32_t(2 * (ncols - cbase)));
+        }
+      }
+    };
+    if (N1024X_RV_EARLY) load_rv();
+
     S16 s;
     // ---- phase 2: IFFT_1024 on this wave's group
     {  // layout A: v = 16*lane + r
@@ -398,27 +423,17 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
     }
 
     // phase-5 operands requested now, consumed after the derivative and the
-    // FFT: E[y] of this lane's erased output rows y = 4 lane + q, and the
-    // received ones (8 B of the row: this group's 4 columns)
+    // FFT: E[y] of this lane's erased output rows y = 4 lane + q (and the
+    // received ones)
     Tab T5[4];
-    uint2 rv[4];
-    {
-      uint32_t ol2 = lane;
-      asm volatile("" : "+v"(ol2));
-      const bool whole = cbase + 4 <= ncols;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t m = (meta[2 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
-        rv[q] = make_uint2(0, 0);
-        // defined on every path (a table read only where used would be carried
-        // across the tile loop, and spilled, by the compiler)
-        load_tab(t.mtab_tout, m != 0xFFFFu ? m : 0u, T5[q]);  // tower in, symbols out
-        if (m == 0xFFFFu) {
-          const uint8_t *row = SH + uint64_t(4 * ol2 + q) * sstride + 2 * cbase;
-          rv[q] = whole ? *reinterpret_cast<const uint2 *>(row) : load8_any(row, uint32_t(2 * (ncols - cbase)));
-        }
-      }
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t m = (meta[2 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
+      // defined on every path (a table read only where used would be carried
+      // across the tile loop, and spilled, by the compiler)
+      load_tab(t.mtab_tout, m != 0xFFFFu ? m : 0u, T5[q]);  // tower in, symbols out
     }
+    if (!N1024X_RV_EARLY) load_rv();
 
     // ---- phases 3 + 4: the closed-form derivative at y < 256 and the FFT
     // restricted to y < 256 (dec_n1024.hip, the same steps)

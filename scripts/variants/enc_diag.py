@@ -19,6 +19,7 @@ that work costs in the real interleaving:
     dnoout  reconstruct_n1024: the output stores dropped (values asm-consumed)
     xnobar, xnogat, xnoout  the same three for reconstruct_n1024x (writes
             OUTDIR/dec_n1024x.hip)
+    xnorv   reconstruct_n1024x: phase 5's re-read of the present rows dropped
     kclk:F  the clk probe in the kernel of csrc file F (its first kernel with
             dynamic LDS), e.g. kclk:enc_k1024.hip (writes OUTDIR/F)
     dclk    the clk probe in reconstruct_n1024 instead (writes OUTDIR/dec_n1024.hip;
@@ -114,6 +115,10 @@ for k in kinds:
         decx = rep(decx, "      if ((meta[0] & 0xffffu) != 0xffffu) load_row(0);\n", "")
         decx = rep(decx, "        if (half == 1 && on) load_row(1);\n", "")
         decx = rep(decx, "        if (on) {  // one divergent branch", "        if (meta[half] == 0x12345678u) {  //")
+        extra["dec_n1024x.hip"] = decx
+    elif k == "xnorv":
+        decx = rep(decx, "          rv[q] = whole ? *reinterpret_cast<const uint2 *>(row) : load8_any(row, uint32_t(2 * (ncols - cbase)));\n",
+                   "          rv[q] = make_uint2(uint32_t(reinterpret_cast<uintptr_t>(row)), q);\n")
         extra["dec_n1024x.hip"] = decx
     elif k == "xnoout":
         decx = rep(decx, "        *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);\n",
