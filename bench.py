@@ -72,17 +72,17 @@ def pmc_traffic(kernel, nv, plen, cnt, batch):
 # A wave counts as active while any of its instructions is issuing, and waves
 # issue to different pipes (VALU, LDS, memory, scalar) in the same cycle, so
 # the sum can exceed 1; the per-wave wait fractions are reported beside it.
-_WAVES_PER_SIMD = {"reconstruct": (("reconstruct_n1024<false>", "reconstruct_n1024"), 2),
-                   "encode": (("encode_k256w", "encode_k256<1024, 0>", "encode_k256<1024>"), 4)}
+_WAVES_PER_SIMD = {"reconstruct": (("reconstruct_n1024x", 3), ("reconstruct_n1024<false>", 2), ("reconstruct_n1024", 2)),
+                   "encode": (("encode_k256w", 4), ("encode_k256<1024, 0>", 4), ("encode_k256<1024>", 4))}
 
 
 def sq_issue(kernel, nv):
     """SQ issue counters of `kernel` from the committed SQ counter summary
-    (scripts/prof_r4.sh + scripts/sq_summary.py, newest profiles/rNN), measured
+    (scripts/prof_r5.sh + scripts/sq_summary.py, newest profiles/rNN), measured
     on the default workload shape (nv = 1024): the kernels are bounded by
     instruction issue, not HBM."""
     import glob
-    names, waves = _WAVES_PER_SIMD.get(kernel, (None, 0))
+    names = _WAVES_PER_SIMD.get(kernel)
     if names is None or nv != 1024:
         return None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "sq_counters.json")),
@@ -90,8 +90,9 @@ def sq_issue(kernel, nv):
         try:
             with open(path) as f:
                 ks = json.load(f)["kernels"]
-            k = next(ks[n] for n in names if n in ks)  # (kernel names by round)
-            return {"waves_per_simd": waves,
+            name, waves = next((n, w) for n, w in names if n in ks)  # (kernel names by round)
+            k = ks[name]
+            return {"kernel": name, "waves_per_simd": waves,
                     "active_inst_any_per_simd": round(k["frac_active_inst_any"] * waves, 3),
                     "active_valu_per_simd": round(k["frac_active_valu"] * waves, 3),
                     "wave_wait_any_frac": round(k["frac_wait_any"], 3),

@@ -10,7 +10,11 @@ reconstruct kernel's 64-B-per-lane row reads (/1.043).  WRITE_SIZE is exact for
 the 16-B-per-lane stores.
   encode:       fetch = raw x 2 (payload reads are 16 B per lane)
   reconstruct:  fetch = raw / 1.043 (reconstruct_n1024 and _n4096 alike: both
-                read 64 B of a row per lane in the gather).  Since r04
+                read 64 B of a row per lane in the gather).  reconstruct_n1024x
+                (round 5) reads 96 B of a row per lane: raw / 1.0017
+                (profiles/r05/fetchcal.txt, k96), and re-reads its present data
+                rows y < k in phase 5 (8 B per lane; L2 hits, see below: no
+                term added).  Since r04
                 reconstruct_n4096 also reads the received output rows y < k
                 (16 B per lane, LDS-DMA) and the 80 KB per-payload output image
                 per tile; those reads count at half weight and are added back as
@@ -36,6 +40,7 @@ thr = (NV - 1) // 3 + 1
 K = 1 << (thr.bit_length() - 1)
 SL = ((P + 2 * K - 1) // (2 * K)) * 2
 KERNELS = {"encode_k256": "encode", "encode_k256w": "encode", "reconstruct_n1024": "reconstruct",
+           "reconstruct_n1024x": "reconstruct",
            "encode_k1024_fused": "encode", "reconstruct_n4096": "reconstruct",
            "encode_gen": "encode", "reconstruct_gen": "reconstruct",
            "encode_g": "encode", "reconstruct_g": "reconstruct", "error_locator_g": "error_locator"}
@@ -53,7 +58,10 @@ def per_launch(path, counter):
     for d, v in val.items():
         for k, short in KERNELS.items():
             if k + "(" in name[d] or k + "<" in name[d]:
-                out[short].append(v * 1024.0)
+                # the 96-B-per-lane gather's FETCH_SIZE is exact to 0.2%:
+                # rescaled here to the 64-B-per-lane units corrected below
+                scale = 1.043 / 1.0017 if (counter == "FETCH_SIZE" and k == "reconstruct_n1024x") else 1.0
+                out[short].append(v * 1024.0 * scale)
     return {k: sum(v) / len(v) for k, v in out.items()}
 
 
