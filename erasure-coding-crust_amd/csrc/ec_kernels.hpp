@@ -136,6 +136,17 @@ hipError_t launch_systematic(const CodeParams &p, const uint8_t *d_shards, size_
                              size_t shard_stride, size_t batch, uint8_t *d_out, size_t out_stride,
                              hipStream_t s, HostSig *sig = nullptr);
 
+// the per-call encode of tiny codes (enc_tiny.hip): n <= kTinyMaxN, payload
+// <= kTinyBytes carried in the kernel arguments, one workgroup, output rows
+// (pitch ostride) written where `out` points (pinned host memory), the
+// completion flag stored by the kernel (sig->fused)
+constexpr int kTinyMaxN = 32;
+constexpr size_t kTinyBytes = 2048;
+bool tiny_applicable(const CodeParams &p, size_t plen, size_t ostride);
+hipError_t launch_encode_tiny(const CodeParams &p, const DevTables &t, const uint8_t *h_payload, size_t plen,
+                              uint8_t *out, size_t ostride, hipStream_t s, HostSig *sig);
+hipError_t warm_encode_tiny(hipStream_t s);  // device set-up: the first launches
+
 // specialised kernels (enc_k256.hip)
 bool k256_applicable(const CodeParams &p);
 // reconstruct_n1024 runs packed (flattened columns, any even shard pitch)

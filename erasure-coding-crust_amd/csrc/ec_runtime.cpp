@@ -199,7 +199,8 @@ DeviceState *device_state() {
   // (ECCR_Test_MeasurePerformance starts its clock after this) pays it
   uint32_t *warm = nullptr;
   if (hipMalloc(&warm, 64) == hipSuccess) {
-    if (launch_signal_host(warm, 1, nullptr) == hipSuccess) (void)hipDeviceSynchronize();
+    if (launch_signal_host(warm, 1, nullptr) == hipSuccess && warm_encode_tiny(nullptr) == hipSuccess)
+      (void)hipDeviceSynchronize();
     (void)hipFree(warm);
   }
   slot = std::move(st);

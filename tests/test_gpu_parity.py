@@ -120,6 +120,17 @@ def test_random_vs_oracle(oracle, nv):
             assert out[:plen] == p
 
 
+def test_tiny_encode_vs_oracle(oracle):
+    """enc_tiny.hip (per-call encode, n <= 32, payload <= 2048 B in the kernel
+    arguments): every n_validators it takes, payload lengths around its piece
+    and size boundaries, and the first lengths past it (the staged path)."""
+    rng = np.random.default_rng(32)
+    for nv in range(2, 34):
+        for plen in (1, 2, 3, 4, 5, 15, 16, 17, 300, 1000, 2047, 2048, 2049):
+            p = rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+            assert E.obtain_chunks(nv, p) == oracle.encode(nv, p), (nv, plen)
+
+
 @pytest.mark.parametrize("nv", [16384, 65536])
 def test_huge_n(oracle, nv):
     n, k, thr = E.code_params(nv)
