@@ -68,10 +68,9 @@ def pmc_traffic(kernel, nv, plen, cnt, batch):
 
 
 # waves per SIMD of the dominant kernels (launch shapes in csrc/): the SQ
-# counters' per-wave ACTIVE_INST_ANY / WAVE_CYCLES summed over a SIMD's waves.
-# A wave counts as active while any of its instructions is issuing, and waves
-# issue to different pipes (VALU, LDS, memory, scalar) in the same cycle, so
-# the sum can exceed 1; the per-wave wait fractions are reported beside it.
+# counters' per-wave VALU instruction rate summed over a SIMD's waves (the
+# VALU instructions one SIMD issued per quad-cycle), and the per-wave wait
+# fractions beside it.
 _WAVES_PER_SIMD = {"reconstruct": (("reconstruct_n1024x", 3), ("reconstruct_n1024<false>", 2), ("reconstruct_n1024", 2)),
                    "encode": (("encode_k256w", 4), ("encode_k256<1024, 0>", 4), ("encode_k256<1024>", 4))}
 
@@ -92,13 +91,18 @@ def sq_issue(kernel, nv):
                 ks = json.load(f)["kernels"]
             name, waves = next((n, w) for n, w in names if n in ks)  # (kernel names by round)
             k = ks[name]
+            # SQ_ACTIVE_INST_VALU equals SQ_INSTS_VALU: it counts instructions
+            # (per quad-cycle of SQ_WAVE_CYCLES), not VALU busy time; the
+            # busy fraction needs per-opcode prices (profiles/r05/*_account.md)
+            per_quad = k["frac_active_valu"] * waves
             return {"kernel": name, "waves_per_simd": waves,
-                    "active_inst_any_per_simd": round(k["frac_active_inst_any"] * waves, 3),
-                    "active_valu_per_simd": round(k["frac_active_valu"] * waves, 3),
+                    "valu_insts_per_simd_quad_cycle": round(per_quad, 3),
+                    "cycles_per_valu_inst": round(4.0 / per_quad, 2) if per_quad else None,
                     "wave_wait_any_frac": round(k["frac_wait_any"], 3),
                     "wave_wait_inst_any_frac": round(k["frac_wait_inst_any"], 3),
                     "measured_in_this_run": False,
-                    "source": os.path.relpath(path, ROOT) + " (stored SQ counter profile)"}
+                    "source": os.path.relpath(path, ROOT) + " (stored SQ counter profile)",
+                    "account": "profiles/r05/enc_valu_account.md, profiles/r05/rec_account.md"}
         except (OSError, KeyError, ValueError, StopIteration):
             continue
     return None
