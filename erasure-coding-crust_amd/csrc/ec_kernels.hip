@@ -561,6 +561,7 @@ hipError_t launch_signal_host(uint32_t *h_flag, uint32_t v, hipStream_t s) {
 size_t encode_scratch_bytes(const CodeParams &p, size_t plen, size_t batch) {
   if (k1024_applicable(p)) return k1024_scratch_bytes(plen, batch);
   if (k256_applicable(p)) return k256_scratch_bytes(p);
+  if (encgen_applicable(p)) return encgen_scratch_bytes(p);
   if (p.k <= uint32_t(kLdsSlots)) return 0;
   const size_t pieces = shard_len(p.k, plen) / 2;
   const size_t tiles = (pieces + 3) / 4;
@@ -581,7 +582,7 @@ hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t 
            : aligned))
     return launch_encode_k256(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
   if (aligned && encgen_applicable(p))
-    return launch_encode_gen(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
+    return launch_encode_gen(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
   if (aligned && scratch && k1024_applicable(p))
     return launch_encode_k1024(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
   const size_t sl = shard_len(p.k, plen);

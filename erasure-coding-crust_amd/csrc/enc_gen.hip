@@ -35,7 +35,8 @@ namespace {
 using namespace tf;
 constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
-constexpr int LDS_BYTES = Tabs::kBytes + WAVES * REG_BYTES;
+constexpr int SLOT = Tabs::kBytes + WAVES * REG_BYTES;  // the next tile's index (dynamic schedule)
+constexpr int LDS_BYTES = SLOT + 16;
 static_assert(LDS_BYTES <= 160 * 1024 && Tabs::kBytes == kTabImageBytes, "LDS budget");
 
 template <int M>
@@ -180,7 +181,7 @@ template <int M>
 __global__ void __launch_bounds__(THREADS)
     encode_gen(const uint8_t *__restrict__ payloads, uint64_t plen, uint64_t pstride,
                uint8_t *__restrict__ shards, uint64_t slen, uint64_t sstride, int nv, int n,
-               uint32_t batch, DevTables t) {
+               uint32_t batch, uint32_t *tick, DevTables t) {
   using Gm = Geo<M>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *tabs = lds;
@@ -201,13 +202,24 @@ __global__ void __launch_bounds__(THREADS)
     }
   };
   // tower images: the transforms run in tower coordinates
+  // Tiles (round 5): a workgroup's first is blockIdx.x, every later one
+  // gridDim.x + a ticket from *tick (zeroed by the launcher), taken by thread
+  // 0 during a tile and published in the LDS word SLOT at its end (read after
+  // the next tile's first barrier).  The static stride gave the workgroups
+  // blockIdx = -1 mod tiles-per-payload every partial last tile (15.27 tiles
+  // per payload at k = 512: ~5% of the launch idle).  tick == nullptr: static.
+  volatile uint32_t *slot = reinterpret_cast<volatile uint32_t *>(lds + SLOT);
+  uint32_t taken = 0;
+  if (tick && tid0 == 0) taken = gridDim.x + atomicAdd(tick, 1u);
   Tabs::copy_image<THREADS>(tabs, t.timg_t, tid0);  // skews 0..1022: every coset of n <= 1024
   __syncthreads();
+  if (tid0 == 0) *slot = taken;
 
   const uint64_t npieces = slen / 2;
   const uint32_t tiles_pp = uint32_t((npieces + Gm::TP - 1) / Gm::TP);
   const uint64_t total = uint64_t(tiles_pp) * batch;
-  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+  uint64_t nxt = 0;
+  for (uint64_t tile = blockIdx.x; tile < total; tile = nxt) {
     uint32_t tid = tid0;
     asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63;
@@ -255,6 +267,8 @@ __global__ void __launch_bounds__(THREADS)
     // the regions (store_rows) sits right before that write, and the stores
     // overlap the register-only first pass that precedes it.
     lds_barrier();  // the other waves are done reading the regions (last tile)
+    nxt = tick ? uint64_t(__builtin_amdgcn_readfirstlane(*slot)) : tile + gridDim.x;
+    if (tick && tid0 == 0) taken = gridDim.x + atomicAdd(tick, 1u);  // the tile after nxt
     stage<M>(s, my, lane);
     lds_barrier();
     store_rows<M>(regions, SH, sstride, 0, nv, piece0, npieces, tid);
@@ -330,6 +344,8 @@ __global__ void __launch_bounds__(THREADS)
       }
       store_rows<M>(regions, SH, sstride, uint32_t(sh), nv, piece0, npieces, tid);
     }
+    // (every wave read SLOT before this tile's second barrier)
+    if (tid0 == 0) *slot = taken;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
 }
@@ -337,7 +353,7 @@ __global__ void __launch_bounds__(THREADS)
 template <int M>
 hipError_t launch_m(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                     size_t plen, size_t pstride, size_t batch, uint8_t *d_shards, size_t sstride,
-                    hipStream_t s) {
+                    void *scratch, hipStream_t s) {
   int cus = 0;
   if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&encode_gen<M>), LDS_BYTES, &cus);
       e != hipSuccess)
@@ -345,9 +361,13 @@ hipError_t launch_m(const CodeParams &p, const DevTables &t, const uint8_t *d_pa
   const size_t sl = shard_len(p.k, plen);
   const size_t tiles = (sl / 2 + Geo<M>::TP - 1) / Geo<M>::TP * batch;
   const unsigned grid = unsigned(tiles < size_t(cus) ? tiles : size_t(cus));
+  // dynamic tiles when the caller gave the counter's scratch (encgen_scratch_bytes)
+  uint32_t *tick = tiles + 2 * size_t(cus) < (size_t(1) << 32) ? static_cast<uint32_t *>(scratch) : nullptr;
+  if (tick)
+    if (const hipError_t e = launch_zero_counters(tick, sizeof(uint32_t), s); e != hipSuccess) return e;
   hipLaunchKernelGGL(encode_gen<M>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
                      uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride),
-                     int(p.nv), int(p.n), uint32_t(batch), t);
+                     int(p.nv), int(p.n), uint32_t(batch), tick, t);
   return hipGetLastError();
 }
 
@@ -357,16 +377,18 @@ bool encgen_applicable(const CodeParams &p) {
   return p.k >= 16 && p.k <= 512 && (p.k & (p.k - 1)) == 0 && p.n <= 4096 && p.n >= 2 * p.k;
 }
 
+size_t encgen_scratch_bytes(const CodeParams &p) { return encgen_applicable(p) ? 256 : 0; }
+
 hipError_t launch_encode_gen(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                              size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
-                             size_t sstride, hipStream_t s) {
+                             size_t sstride, void *scratch, hipStream_t s) {
   switch (p.k) {
-    case 16: return launch_m<4>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
-    case 32: return launch_m<5>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
-    case 64: return launch_m<6>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
-    case 128: return launch_m<7>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
-    case 256: return launch_m<8>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
-    default: return launch_m<9>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, s);
+    case 16: return launch_m<4>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
+    case 32: return launch_m<5>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
+    case 64: return launch_m<6>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
+    case 128: return launch_m<7>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
+    case 256: return launch_m<8>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
+    default: return launch_m<9>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
   }
 }
 
