@@ -84,6 +84,9 @@ __device__ __forceinline__ void tab_f9(uint32_t s, uint32_t c, F9Tab &T) {
 constexpr int tk(int k) { return k < 8 ? 0 : k < 12 ? 1 : k < 14 ? 2 : 3; }
 constexpr int bk(int k) { return k < 8 ? 2 * k : k < 12 ? 4 * (k - 8) : k < 14 ? 8 * (k - 12) : 0; }
 
+#ifndef N1024X_RV_EARLY
+#define N1024X_RV_EARLY 1
+#endif
 #ifndef N1024X_RA
 #define N1024X_RA 2
 #endif
@@ -261,65 +264,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
     }
   };
   uint32_t meta[4] = {0, 0, 0, 0}, meta_next[4] = {0, 0, 0, 0};
-  // ---- phase 1 of tile tl: gather + scale this thread's slots' rows
-  // (decode_main:174-177), 12 groups of 4 columns each into the groups'
-  // regions; absent rows as 0.  Runs right after the thread's own phase 5 of
-  // the previous tile, while the other waves may still be in their FFT: the
-  // regions are free since every wave passed barrier Y (below).
-  const auto gather = [&](uint32_t tl) __attribute__((always_inline)) {
-    uint32_t tid = tid0;
-    asm volatile("" : "+v"(tid));
-    const uint32_t bq = tl / tiles_pp;
-    const uint64_t col0 = uint64_t(tl - bq * tiles_pp) * COLS;
-    const uint8_t *SH = shards + uint64_t(bq) * uint64_t(nv) * sstride;
-    uint32_t w[ROW_WORDS] = {};  // (defined on every path: not carried across tiles)
-    Tab RT = {};
-    const uint64_t avail = slen - 2 * col0;  // bytes of a row inside the tile
-    const auto load_row = [&](int half) __attribute__((always_inline)) {
-      const uint8_t *row = SH + uint64_t(meta[half] >> 16) * sstride + 2 * col0;
-      if (avail >= 2 * COLS) {
-#pragma unroll
-        for (int q = 0; q < ROW_WORDS / 4; ++q) {
-          const uint4 d = reinterpret_cast<const uint4 *>(row)[q];
-          w[4 * q] = d.x;
-          w[4 * q + 1] = d.y;
-          w[4 * q + 2] = d.z;
-          w[4 * q + 3] = d.w;
-        }
-      } else {  // the payload's last tile
-        load_row_tail96(row, uint32_t(avail), w);
-      }
-      load_tab(t.mtab_tin, meta[half] & 0xffffu, RT);  // scaled into tower coordinates
-    };
-    if ((meta[0] & 0xffffu) != 0xffffu) load_row(0);
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      if (half == 1 && tid >= uint32_t(N - THREADS)) break;  // (uniform per wave)
-      const uint32_t v = meta[half] >> 16;
-      const bool on = (meta[half] & 0xffffu) != 0xffffu;
-      if (half == 1 && on) load_row(1);
-      uint32_t l[WAVES], h[WAVES];
-#pragma unroll
-      for (int g = 0; g < WAVES; ++g) l[g] = h[g] = 0;
-      if (on) {  // one divergent branch for the 12 groups
-#pragma unroll
-        for (int g = 0; g < WAVES; ++g) {  // columns 4g..4g+3: words (h0 l0 h1 l1)(h2 l2 h3 l3)
-          const uint32_t a = w[2 * g], c = w[2 * g + 1];
-          const uint32_t xh = vperm(c, a, 0x06040200u), xl = vperm(c, a, 0x07050301u);
-          mul_acc(xl, xh, RT, l[g], h[g]);
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < WAVES; ++g)
-        *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l[g], h[g]);
-    }
-  };
   uint32_t cur = blockIdx.x;  // (total < 2^32: launcher)
-  if (cur < total) {
-    load_meta(cur / tiles_pp, tid0, meta);
-    gather(cur);
-  }
-  __syncthreads();  // X: the regions hold the first tile
+  if (cur < total) load_meta(cur / tiles_pp, tid0, meta);
   while (cur < total) {
     // lane-derived addresses recomputed per tile (not hoisted and spilled)
     uint32_t tid = tid0;
@@ -329,23 +275,76 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
     const uint64_t b = bq, col0 = uint64_t(cur - bq * tiles_pp) * COLS;
     const uint8_t *SH = shards + b * uint64_t(nv) * sstride;
     uint8_t *O = out + b * ostride;
-    const uint32_t nxt = __builtin_amdgcn_readfirstlane(*slot);  // the next tile (SLOT)
-    if (tid0 == 0) taken = gridDim.x + atomicAdd(tick, 1u);  // the tile after nxt
+
+    uint32_t nxt;  // the next tile (SLOT)
+    // ---- phase 1: gather + scale this thread's slots' rows (decode_main:
+    // 174-177), 12 groups of 4 columns each into the groups' regions; absent
+    // rows as 0.  The first slot's row and E[v] table are requested before
+    // the tile barrier.
+    {
+      uint32_t w[ROW_WORDS] = {};  // (defined on every path: not carried across tiles)
+      Tab RT = {};
+      const uint64_t avail = slen - 2 * col0;  // bytes of a row inside the tile
+      const auto load_row = [&](int half) __attribute__((always_inline)) {
+        const uint8_t *row = SH + uint64_t(meta[half] >> 16) * sstride + 2 * col0;
+        if (avail >= 2 * COLS) {
+#pragma unroll
+          for (int q = 0; q < ROW_WORDS / 4; ++q) {
+            const uint4 d = reinterpret_cast<const uint4 *>(row)[q];
+            w[4 * q] = d.x;
+            w[4 * q + 1] = d.y;
+            w[4 * q + 2] = d.z;
+            w[4 * q + 3] = d.w;
+          }
+        } else {  // the payload's last tile
+          load_row_tail96(row, uint32_t(avail), w);
+        }
+        load_tab(t.mtab_tin, meta[half] & 0xffffu, RT);  // scaled into tower coordinates
+      };
+      if ((meta[0] & 0xffffu) != 0xffffu) load_row(0);
+      lds_barrier();  // the previous tile's readers of the regions are done
+      nxt = __builtin_amdgcn_readfirstlane(*slot);
+      if (tid0 == 0) taken = gridDim.x + atomicAdd(tick, 1u);  // the tile after nxt
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        if (half == 1 && tid >= uint32_t(N - THREADS)) break;  // (uniform per wave)
+        const uint32_t v = meta[half] >> 16;
+        const bool on = (meta[half] & 0xffffu) != 0xffffu;
+        if (half == 1 && on) load_row(1);
+        uint32_t l[WAVES], h[WAVES];
+#pragma unroll
+        for (int g = 0; g < WAVES; ++g) l[g] = h[g] = 0;
+        if (on) {  // one divergent branch for the 12 groups
+#pragma unroll
+          for (int g = 0; g < WAVES; ++g) {  // columns 4g..4g+3: words (h0 l0 h1 l1)(h2 l2 h3 l3)
+            const uint32_t a = w[2 * g], c = w[2 * g + 1];
+            const uint32_t xh = vperm(c, a, 0x06040200u), xl = vperm(c, a, 0x07050301u);
+            mul_acc(xl, xh, RT, l[g], h[g]);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < WAVES; ++g)
+          *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l[g], h[g]);
+      }
+    }
     if (nxt < total) load_meta(nxt / tiles_pp, tid, meta_next);
+    __syncthreads();  // (every wave has read SLOT)
     const uint64_t cbase = col0 + 4 * uint64_t(wave_s);  // wave-uniform
     // a group past the payload's last column (the last, partial tile: 1 MB is
-    // 1954 columns, the 41st tile has 34) computes nothing, but takes part in
-    // the barriers and the next gather
-    const bool active = cbase < ncols;
-    S16 s;
-    uint2 rv[4];
-    uint32_t lc = 0;
-    if (active) {
+    // 1954 columns, the 41st tile has 34): phases 2-5 are this wave's alone
+    if (cbase >= ncols) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) meta[i] = meta_next[i];
+      cur = nxt;
+      continue;
+    }
+
     // phase 5's received rows y = 4 lane + q < 256 (8 B of the row: this
     // group's 4 columns), re-read from the shards (L2: the gather has just
     // read them; no LDS left to stage them), requested before the IFFT
-    // (A/B at B = 4096 against requesting them after it: 10.68 / 10.92 ms
+    // (N1024X_RV_EARLY = 0: after it; A/B at B = 4096: 10.68 / 10.92 ms
     // against 10.76 / 11.00, and 154 VGPRs instead of 168)
+    uint2 rv[4];
     const auto load_rv = [&]() __attribute__((always_inline)) {
       uint32_t ol2 = lane;
       asm volatile("" : "+v"(ol2));
@@ -360,8 +359,9 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
         }
       }
     };
-    load_rv();
+    if (N1024X_RV_EARLY) load_rv();
 
+    S16 s;
     // ---- phase 2: IFFT_1024 on this wave's group
     {  // layout A: v = 16*lane + r
       const uint32_t la = lds_addr(my) | raddr(16 * lane);
@@ -396,17 +396,13 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
     }
     prio3(wave_s, 2);
     // layout C: r bit0 = p8, bit1 = p9, bit2 = p6, bit3 = p7; lane = p0..p5
-    lc = lds_addr(my) | raddr(lane);
+    const uint32_t lc = lds_addr(my) | raddr(lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const uint2 x = lds_ld2(lc ^ raddr((uint32_t((r >> 2) & 3) << 6) | (uint32_t(r & 3) << 8)));
       s.l[r] = x.x;
       s.h[r] = x.y;
     }
-    }  // active, part 1
-    lds_barrier();  // Y: every wave is done with the regions (layout C read)
-    if (tid0 == 0) *slot = taken;  // (every wave has read SLOT since barrier X)
-    if (active) {
     // IFFT stages 8 and 9 (index 0): stage 9 is b ^= a only, stage 8
     // multiplies in its p9 = 1 block only (dec_n1024.hip)
     {
@@ -437,6 +433,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
       // across the tile loop, and spilled, by the compiler)
       load_tab(t.mtab_tout, m != 0xFFFFu ? m : 0u, T5[q]);  // tower in, symbols out
     }
+    if (!N1024X_RV_EARLY) load_rv();
 
     // ---- phases 3 + 4: the closed-form derivative at y < 256 and the FFT
     // restricted to y < 256 (dec_n1024.hip, the same steps)
@@ -579,12 +576,12 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
         *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);
       }
     }
-    }  // active, part 2
+    // thread 0 (wave 0 never idles: its columns start the tile) publishes the
+    // tile after next; the atomic returned during the transform
+    if (tid0 == 0) *slot = taken;
 #pragma unroll
     for (int i = 0; i < 4; ++i) meta[i] = meta_next[i];
     cur = nxt;
-    if (cur < total) gather(cur);
-    __syncthreads();  // X: the regions hold the next tile
   }
 }
 
