@@ -596,10 +596,11 @@ def test_batch_random_shapes_and_runs(oracle, seed):
 
 
 @pytest.mark.parametrize("nv,plen,pad", [
-    (1024, 70001, 64), (800, 33333, 16),                # reconstruct_n1024 (nv = n and nv < n)
+    (1024, 70001, 64), (800, 33333, 16),                # reconstruct_n1024x, k = 256 (nv = n and nv < n)
     (1500, 70001, 64), (2048, 40001, 16),               # reconstruct_n4096, 2 halves, k = 256 / 512
     (2500, 70001, 64), (3070, 90001, 16), (4096, 70001, 64),  # 4 quarters, k = 512 / 1024
-    (600, 50001, 64), (300, 20001, 16), (100, 9999, 16), (46, 5001, 64),  # reconstruct_gen
+    (600, 50001, 64), (513, 70001, 64), (765, 40001, 16),  # reconstruct_gen, n = 1024, k = 128
+    (600, 9001, 64), (300, 20001, 16), (100, 9999, 16), (46, 5001, 64),  # reconstruct_gen
     (6, 3001, 0), (20, 999, 0), (5000, 40001, 0)])     # generic kernels (incl. n = 8192)
 def test_batch_patterns_every_kernel(oracle, nv, plen, pad):
     """Device batch reconstruct through ECCR_AMD_reconstruct_batch with every
