@@ -151,7 +151,11 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
                             "H2D"))
     return false;
   HostSig sig = direct ? call_signal(c) : HostSig();
-  if (all_systematic) {
+  if (all_systematic && direct && systematic_tiny_applicable(p, sl)) {
+    // tiny calls: the k systematic shards ride in the kernel arguments (enc_tiny.hip)
+    if (!hip_check(launch_systematic_tiny(p, c->h_in, sl, dstride, dst, c->stream, &sig), "systematic launch"))
+      return false;
+  } else if (all_systematic) {
     // every systematic shard is present: decode == interleave (exact)
     if (!hip_check(launch_systematic(p, src, sl, dstride, 1, dst, out_bytes, c->stream, &sig),
                    "systematic launch"))

@@ -137,15 +137,21 @@ hipError_t launch_systematic(const CodeParams &p, const uint8_t *d_shards, size_
                              hipStream_t s, HostSig *sig = nullptr);
 
 // the per-call encode of tiny codes (enc_tiny.hip): n <= kTinyMaxN, payload
-// <= kTinyBytes carried in the kernel arguments, one workgroup, output rows
+// <= kTinyBytes and the code's tables carried in the kernel arguments, one workgroup, output rows
 // (pitch ostride) written where `out` points (pinned host memory), the
 // completion flag stored by the kernel (sig->fused)
-constexpr int kTinyMaxN = 32;
+constexpr int kTinyMaxN = 16;
 constexpr size_t kTinyBytes = 2048;
 bool tiny_applicable(const CodeParams &p, size_t plen, size_t ostride);
 hipError_t launch_encode_tiny(const CodeParams &p, const DevTables &t, const uint8_t *h_payload, size_t plen,
                               uint8_t *out, size_t ostride, hipStream_t s, HostSig *sig);
-hipError_t warm_encode_tiny(hipStream_t s);  // device set-up: the first launches
+// the per-call decode from all k systematic shards of a tiny call (k * slen <=
+// kTinyBytes, shards at h_shards with pitch sstride, read on the host into the
+// kernel arguments): out = the interleaved payload (pinned), flag by the kernel
+bool systematic_tiny_applicable(const CodeParams &p, size_t slen);
+hipError_t launch_systematic_tiny(const CodeParams &p, const uint8_t *h_shards, size_t slen, size_t sstride,
+                                  uint8_t *out, hipStream_t s, HostSig *sig);
+hipError_t warm_encode_tiny(hipStream_t s);  // device set-up: the first launches of the tiny kernels
 
 // specialised kernels (enc_k256.hip)
 bool k256_applicable(const CodeParams &p);

@@ -1,5 +1,5 @@
 // enc_tiny.hip — the per-call C ABI's encode for tiny codes and payloads
-// (n <= 32, i.e. n_validators <= 32; payload <= kTinyBytes): the shape of the
+// (n <= 16, i.e. n_validators <= 16; payload <= kTinyBytes): the shape of the
 // reference's own benchmark (`benchmark/benchmark.cpp:15`, n_validators = 6,
 // 15 B .. 5 KB payloads through ECCR_Test_MeasurePerformance).
 //
@@ -8,8 +8,8 @@
 // pinned host memory +0.7-1.1 us).  So:
 //  * the payload travels in the kernel arguments (no host-memory reads, no
 //    host-side copy into the staging buffer);
-//  * the code's skew tables (n - 1 of them, mslot[0 .. n-2]) are fetched in
-//    one parallel step into LDS;
+//  * so do the code's skew tables (n - 1 <= 15 of them, mslot[0 .. n-2],
+//    built on the host): no dependent device-memory round trip, no LDS;
 //  * one thread per piece keeps its k <= 8 symbols in registers through the
 //    IFFT_k and each coset's FFT_k (additive_fft.hpp:99-141; encodeLow,
 //    poly_encoder.hpp:217-240), and writes its 2-byte BE symbol of every shard
@@ -17,8 +17,13 @@
 //    bytes of a row);
 //  * the same workgroup stores the completion flag (HostSig).
 // The multiply is mul_acc on byte-planar words with the symbol in byte 0.
+// systematic_tiny is the same for the per-call decode from all k systematic
+// shards (reed-solomon.hpp:143-179): the k shards (<= kTinyBytes together) in
+// the kernel arguments, the interleaved payload written to the pinned output.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <array>
 #include <cstring>
 #include <type_traits>
 
@@ -29,7 +34,7 @@ namespace ecamd {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kLogMaxK = 3;
+constexpr int kLogMaxK = 2;  // n <= 16: k <= 4
 constexpr int kMaxK = 1 << kLogMaxK;
 
 // PB: payload bytes carried (the argument block is copied at every launch:
@@ -39,23 +44,35 @@ struct TinyArgs {
   uint32_t w[PB / 4];
 };
 
+// the code's multiply tables, mslot[0 .. n-2] (every skew of IFFT_k at 0 and
+// FFT_k at the cosets below n), in the kernel arguments too
+struct TinyTabs {
+  MulTab t[kTinyMaxN - 1];
+};
+
 template <int PB>
-__global__ void __launch_bounds__(kThreads) encode_tiny(TinyArgs<PB> pay, uint32_t plen, uint32_t nv,
-                                                         uint32_t n, uint32_t logk, uint32_t npieces,
+__global__ void __launch_bounds__(kThreads) encode_tiny(TinyArgs<PB> pay, TinyTabs tt, uint32_t nv, uint32_t n,
+                                                         uint32_t logk, uint32_t npieces,
                                                          uint8_t *__restrict__ out, uint64_t ostride,
-                                                         const MulTab *__restrict__ mslot,
                                                          uint32_t *sig_flag, uint32_t sig_v) {
-  __shared__ MulTab tabs[kTinyMaxN];
-  __shared__ uint32_t pw[PB / 4];
   const uint32_t tid = threadIdx.x, k = 1u << logk;
-  // one parallel round of loads: the tables (skew slots 0 .. n-2, every
-  // table of the code) and the payload's words out of the kernel arguments
-  // into LDS (byte loads from the arguments, one per symbol byte, were a
-  // chain of dependent round trips)
-  if (tid < n - 1) tabs[tid] = mslot[tid];
-  for (uint32_t i = tid; i < (plen + 3) / 4; i += kThreads) pw[i] = pay.w[i];
+  // the tables into LDS in one parallel round of loads from the arguments
+  // (read where used instead, each multiply waited for its own load)
+  __shared__ MulTab tabs[kTinyMaxN - 1];
+  if (tid < 5 * (n - 1))
+    reinterpret_cast<uint4 *>(tabs)[tid] = reinterpret_cast<const uint4 *>(tt.t)[tid];
+  // piece p = symbols p*k .. p*k + k - 1, BE (poly_encoder.hpp:53-76):
+  // bytes [2pk, 2pk + 2k), zero past the payload (the host pads the
+  // arguments), from two unconditional word loads; the first piece's are
+  // requested with the tables, before the barrier
+  uint32_t q0 = 0, q1 = 0;
+  const auto words = [&](uint32_t p) {
+    const uint32_t w0 = 2 * p * k / 4;
+    q0 = pay.w[w0 < PB / 4 ? w0 : PB / 4 - 1];
+    q1 = pay.w[w0 + 1 < PB / 4 ? w0 + 1 : PB / 4 - 1];
+  };
+  if (tid < npieces) words(tid);
   __syncthreads();
-  const uint8_t *P = reinterpret_cast<const uint8_t *>(pw);
   const auto tab = [&](uint32_t i, Tab &T) {
     const uint4 *q = reinterpret_cast<const uint4 *>(&tabs[i]);
 #pragma unroll
@@ -72,18 +89,15 @@ __global__ void __launch_bounds__(kThreads) encode_tiny(TinyArgs<PB> pay, uint32
     *reinterpret_cast<uint16_t *>(out + uint64_t(r) * ostride + 2 * p) = uint16_t(hi | (lo << 8));
   };
   for (uint32_t p = tid; p < npieces; p += kThreads) {
-    // piece p = symbols p*k .. p*k + k - 1, BE, zero past the payload
-    // (poly_encoder.hpp:53-76); symbol in byte 0 of (l, h)
+    const uint32_t b0 = 2 * p * k;
+    const uint64_t q = (uint64_t(q1) << 32 | q0) >> (8 * (b0 & 3));
+    if (p + kThreads < npieces) words(p + kThreads);  // the next piece of this thread
     uint32_t cl[kMaxK], ch[kMaxK];
 #pragma unroll
-    for (int i = 0; i < kMaxK; ++i) {
-      cl[i] = ch[i] = 0;
-      if (uint32_t(i) < k) {
-        const uint32_t off = 2 * (p * k + i);
-        ch[i] = off < plen ? P[off] : 0u;
-        cl[i] = off + 1 < plen ? P[off + 1] : 0u;
-        if (uint32_t(i) < nv) put(i, p, cl[i], ch[i]);  // systematic rows
-      }
+    for (int i = 0; i < kMaxK; ++i) {  // symbol in byte 0 of (l, h)
+      ch[i] = uint32_t(q >> (16 * i)) & 0xFFu;
+      cl[i] = uint32_t(q >> (16 * i + 8)) & 0xFFu;
+      if (uint32_t(i) < k) put(i, p, cl[i], ch[i]);  // systematic rows (k <= nv)
     }
     // IFFT_k at index 0: b ^= a; a ^= b * skew  (stage m, block skew j - 1)
     // (stages and registers compile-time: no dynamic register indexing)
@@ -137,6 +151,24 @@ __global__ void __launch_bounds__(kThreads) encode_tiny(TinyArgs<PB> pay, uint32
   if (tid == 0 && sig_flag) __hip_atomic_store(sig_flag, sig_v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+template <int PB>
+__global__ void __launch_bounds__(kThreads) systematic_tiny(TinyArgs<PB> sh, uint32_t slen, uint32_t logk,
+                                                             uint8_t *__restrict__ out, uint32_t *sig_flag,
+                                                             uint32_t sig_v) {
+  // shard y's bytes at sh[y * slen ..]; out[2 (i k + y) ..] = shard_y[2 i ..]
+  const uint8_t *S = reinterpret_cast<const uint8_t *>(sh.w);
+  const uint32_t k = 1u << logk, total = (slen / 2) * k;
+  for (uint32_t e = threadIdx.x; e < total; e += kThreads) {
+    const uint32_t i = e >> logk, y = e & (k - 1);
+    const uint32_t a = y * slen + 2 * i;
+    *reinterpret_cast<uint16_t *>(out + 2 * e) = uint16_t(S[a] | (uint32_t(S[a + 1]) << 8));
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0 && sig_flag)
+    __hip_atomic_store(sig_flag, sig_v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace
 
 bool tiny_applicable(const CodeParams &p, size_t plen, size_t ostride) {
@@ -144,21 +176,63 @@ bool tiny_applicable(const CodeParams &p, size_t plen, size_t ostride) {
          ostride % 2 == 0;
 }
 
+namespace {
+// the code's tables, built once per n on the host (mslot[i] = mtab[skews[i]])
+const TinyTabs &tiny_tabs(uint32_t n) {
+  static const std::array<TinyTabs, 5> all = [] {
+    std::array<TinyTabs, 5> a{};
+    const Field &f = field();
+    for (int lg = 0; lg < 5; ++lg)
+      for (uint32_t i = 0; i + 1 < (1u << lg); ++i) a[lg].t[i] = f.mtab[f.skews[i]];
+    return a;
+  }();
+  return all[__builtin_ctz(n)];
+}
+}  // namespace
+
 hipError_t launch_encode_tiny(const CodeParams &p, const DevTables &t, const uint8_t *h_payload, size_t plen,
                               uint8_t *out, size_t ostride, hipStream_t s, HostSig *sig) {
   if (!tiny_applicable(p, plen, ostride) || !out || !h_payload) return hipErrorInvalidValue;
   const uint32_t logk = uint32_t(__builtin_ctz(p.k));
   const uint32_t npieces = uint32_t(shard_len(p.k, plen) / 2);
+  const TinyTabs &tt = tiny_tabs(p.n);
   const auto go = [&](auto tag) {
     constexpr int PB = decltype(tag)::value;
     TinyArgs<PB> pay;
-    pay.w[(plen - 1) / 4] = 0;  // (the bytes past plen in the last word: read, unused)
+    // zero past the payload: the last piece's padding and the words a load
+    // may read beyond it (clamped to the block)
+    const size_t pad_end = std::min(size_t(PB), size_t(2) * p.k * npieces + 8);
     std::memcpy(pay.w, h_payload, plen);
-    hipLaunchKernelGGL(encode_tiny<PB>, dim3(1), dim3(kThreads), 0, s, pay, uint32_t(plen), p.nv, p.n, logk,
-                       npieces, out, uint64_t(ostride), t.mslot, sig ? sig->flag : nullptr, sig ? sig->v : 0u);
+    if (pad_end > plen) std::memset(reinterpret_cast<uint8_t *>(pay.w) + plen, 0, pad_end - plen);
+    hipLaunchKernelGGL(encode_tiny<PB>, dim3(1), dim3(kThreads), 0, s, pay, tt, p.nv, p.n, logk, npieces, out,
+                       uint64_t(ostride), sig ? sig->flag : nullptr, sig ? sig->v : 0u);
   };
   if (plen <= 64) go(std::integral_constant<int, 64>());
   else if (plen <= 512) go(std::integral_constant<int, 512>());
+  else go(std::integral_constant<int, int(kTinyBytes)>());
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess && sig && sig->flag) sig->fused = true;
+  return e;
+}
+
+bool systematic_tiny_applicable(const CodeParams &p, size_t slen) {
+  return slen >= 2 && slen % 2 == 0 && size_t(p.k) * slen <= kTinyBytes;
+}
+
+hipError_t launch_systematic_tiny(const CodeParams &p, const uint8_t *h_shards, size_t slen, size_t sstride,
+                                  uint8_t *out, hipStream_t s, HostSig *sig) {
+  if (!systematic_tiny_applicable(p, slen) || !out || !h_shards) return hipErrorInvalidValue;
+  const size_t bytes = size_t(p.k) * slen;
+  const uint32_t logk = uint32_t(__builtin_ctz(p.k));
+  const auto go = [&](auto tag) {
+    constexpr int PB = decltype(tag)::value;
+    TinyArgs<PB> a;
+    for (uint32_t y = 0; y < p.k; ++y) std::memcpy(reinterpret_cast<uint8_t *>(a.w) + y * slen, h_shards + y * sstride, slen);
+    hipLaunchKernelGGL(systematic_tiny<PB>, dim3(1), dim3(kThreads), 0, s, a, uint32_t(slen), logk, out,
+                       sig ? sig->flag : nullptr, sig ? sig->v : 0u);
+  };
+  if (bytes <= 64) go(std::integral_constant<int, 64>());
+  else if (bytes <= 512) go(std::integral_constant<int, 512>());
   else go(std::integral_constant<int, int(kTinyBytes)>());
   const hipError_t e = hipGetLastError();
   if (e == hipSuccess && sig && sig->flag) sig->fused = true;
@@ -174,12 +248,21 @@ hipError_t warm_encode_tiny(hipStream_t s) {
     constexpr int PB = decltype(tag)::value;
     TinyArgs<PB> pay;
     pay.w[0] = 0;
-    hipLaunchKernelGGL(encode_tiny<PB>, dim3(1), dim3(kThreads), 0, s, pay, 1u, 2u, 1u, 0u, 0u, nullptr,
-                       uint64_t(0), nullptr, nullptr, 0u);
+    hipLaunchKernelGGL(encode_tiny<PB>, dim3(1), dim3(kThreads), 0, s, pay, tiny_tabs(2), 2u, 2u, 0u, 0u, nullptr,
+                       uint64_t(0), nullptr, 0u);
   };
   go(std::integral_constant<int, 64>());
   go(std::integral_constant<int, 512>());
   go(std::integral_constant<int, int(kTinyBytes)>());
+  const auto gs = [&](auto tag) {
+    constexpr int PB = decltype(tag)::value;
+    TinyArgs<PB> a;
+    a.w[0] = 0;
+    hipLaunchKernelGGL(systematic_tiny<PB>, dim3(1), dim3(kThreads), 0, s, a, 0u, 0u, nullptr, nullptr, 0u);
+  };
+  gs(std::integral_constant<int, 64>());
+  gs(std::integral_constant<int, 512>());
+  gs(std::integral_constant<int, int(kTinyBytes)>());
   return hipGetLastError();
 }
 

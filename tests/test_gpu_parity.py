@@ -121,7 +121,7 @@ def test_random_vs_oracle(oracle, nv):
 
 
 def test_tiny_encode_vs_oracle(oracle):
-    """enc_tiny.hip (per-call encode, n <= 32, payload <= 2048 B in the kernel
+    """enc_tiny.hip (per-call encode, n <= 16, payload <= 2048 B in the kernel
     arguments): every n_validators it takes, payload lengths around its piece
     and size boundaries, and the first lengths past it (the staged path)."""
     rng = np.random.default_rng(32)
