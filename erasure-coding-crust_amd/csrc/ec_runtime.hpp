@@ -138,13 +138,21 @@ HostCtx *host_ctx();  // nullptr if no device
 // to kFinishSpinUs, then falls back to hipStreamSynchronize (which also
 // reports an asynchronous error).  False (error set) on a HIP error.
 // Every kFinishProbeEvery-th spin-completed call also queries the stream, so
-// an asynchronous kernel error is reported within that many calls.
+// an asynchronous kernel error is reported within that many calls.  (A kernel
+// that faults never stores the word, so its call times out of the spin into
+// hipStreamSynchronize and reports the error itself; the probe is for the
+// rest.  A hipStreamQuery costs ~10 us, so every 16th call, as until round 5,
+// put 12-20 us outliers into the per-call times: scripts/micro/mp_calls.cpp,
+// encode 844-899 -> 761-804 us per 100 calls at 1024.)
 // sig: the completion word and sequence number of the call (call_signal),
 // offered to the call's last kernel launch first: if that kernel stored it
 // itself (HostSig::fused, a single-workgroup launch), no signal kernel is
 // launched.
 constexpr double kFinishSpinUs = 200.0;
-constexpr uint32_t kFinishProbeEvery = 16;
+#ifndef ECCR_PROBE_EVERY
+#define ECCR_PROBE_EVERY 1024
+#endif
+constexpr uint32_t kFinishProbeEvery = ECCR_PROBE_EVERY;
 bool finish_call(HostCtx *c, const char *what, const HostSig *sig = nullptr);
 // the next completion word / value of this context (flag null if the pinned
 // word could not be allocated: finish_call then synchronises the stream)
