@@ -59,8 +59,8 @@ __global__ void __launch_bounds__(kThreads) encode_tiny(TinyArgs<PB> pay, TinyTa
   // the tables into LDS in one parallel round of loads from the arguments
   // (read where used instead, each multiply waited for its own load)
   __shared__ MulTab tabs[kTinyMaxN - 1];
-  if (tid < 5 * (n - 1))
-    reinterpret_cast<uint4 *>(tabs)[tid] = reinterpret_cast<const uint4 *>(tt.t)[tid];
+  for (uint32_t i = tid; i < 5 * (n - 1); i += blockDim.x)  // (75 chunks at n = 16: more than a wave)
+    reinterpret_cast<uint4 *>(tabs)[i] = reinterpret_cast<const uint4 *>(tt.t)[i];
   // piece p = symbols p*k .. p*k + k - 1, BE (poly_encoder.hpp:53-76):
   // bytes [2pk, 2pk + 2k), zero past the payload (the host pads the
   // arguments), from two unconditional word loads; the first piece's are
@@ -88,10 +88,11 @@ __global__ void __launch_bounds__(kThreads) encode_tiny(TinyArgs<PB> pay, TinyTa
   const auto put = [&](uint32_t r, uint32_t p, uint32_t lo, uint32_t hi) {
     *reinterpret_cast<uint16_t *>(out + uint64_t(r) * ostride + 2 * p) = uint16_t(hi | (lo << 8));
   };
-  for (uint32_t p = tid; p < npieces; p += kThreads) {
+  const uint32_t nth = blockDim.x;  // 64 .. kThreads: the pieces, rounded up to whole waves
+  for (uint32_t p = tid; p < npieces; p += nth) {
     const uint32_t b0 = 2 * p * k;
     const uint64_t q = (uint64_t(q1) << 32 | q0) >> (8 * (b0 & 3));
-    if (p + kThreads < npieces) words(p + kThreads);  // the next piece of this thread
+    if (p + nth < npieces) words(p + nth);  // the next piece of this thread
     uint32_t cl[kMaxK], ch[kMaxK];
 #pragma unroll
     for (int i = 0; i < kMaxK; ++i) {  // symbol in byte 0 of (l, h)
@@ -158,7 +159,7 @@ __global__ void __launch_bounds__(kThreads) systematic_tiny(TinyArgs<PB> sh, uin
   // shard y's bytes at sh[y * slen ..]; out[2 (i k + y) ..] = shard_y[2 i ..]
   const uint8_t *S = reinterpret_cast<const uint8_t *>(sh.w);
   const uint32_t k = 1u << logk, total = (slen / 2) * k;
-  for (uint32_t e = threadIdx.x; e < total; e += kThreads) {
+  for (uint32_t e = threadIdx.x; e < total; e += blockDim.x) {
     const uint32_t i = e >> logk, y = e & (k - 1);
     const uint32_t a = y * slen + 2 * i;
     *reinterpret_cast<uint16_t *>(out + 2 * e) = uint16_t(S[a] | (uint32_t(S[a + 1]) << 8));
@@ -167,6 +168,13 @@ __global__ void __launch_bounds__(kThreads) systematic_tiny(TinyArgs<PB> sh, uin
   __syncthreads();
   if (threadIdx.x == 0 && sig_flag)
     __hip_atomic_store(sig_flag, sig_v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// one thread per piece (output symbol), whole waves, at most kThreads: a
+// 15-B call is one wave instead of four
+uint32_t block_for(uint32_t items) {
+  const uint32_t w = (items + 63) / 64 * 64;
+  return w < 64 ? 64 : w > uint32_t(kThreads) ? uint32_t(kThreads) : w;
 }
 
 }  // namespace
@@ -204,7 +212,7 @@ hipError_t launch_encode_tiny(const CodeParams &p, const DevTables &t, const uin
     const size_t pad_end = std::min(size_t(PB), size_t(2) * p.k * npieces + 8);
     std::memcpy(pay.w, h_payload, plen);
     if (pad_end > plen) std::memset(reinterpret_cast<uint8_t *>(pay.w) + plen, 0, pad_end - plen);
-    hipLaunchKernelGGL(encode_tiny<PB>, dim3(1), dim3(kThreads), 0, s, pay, tt, p.nv, p.n, logk, npieces, out,
+    hipLaunchKernelGGL(encode_tiny<PB>, dim3(1), dim3(block_for(npieces)), 0, s, pay, tt, p.nv, p.n, logk, npieces, out,
                        uint64_t(ostride), sig ? sig->flag : nullptr, sig ? sig->v : 0u);
   };
   if (plen <= 64) go(std::integral_constant<int, 64>());
@@ -228,7 +236,8 @@ hipError_t launch_systematic_tiny(const CodeParams &p, const uint8_t *h_shards, 
     constexpr int PB = decltype(tag)::value;
     TinyArgs<PB> a;
     for (uint32_t y = 0; y < p.k; ++y) std::memcpy(reinterpret_cast<uint8_t *>(a.w) + y * slen, h_shards + y * sstride, slen);
-    hipLaunchKernelGGL(systematic_tiny<PB>, dim3(1), dim3(kThreads), 0, s, a, uint32_t(slen), logk, out,
+    hipLaunchKernelGGL(systematic_tiny<PB>, dim3(1), dim3(block_for(uint32_t(slen / 2) * p.k)), 0, s, a,
+                       uint32_t(slen), logk, out,
                        sig ? sig->flag : nullptr, sig ? sig->v : 0u);
   };
   if (bytes <= 64) go(std::integral_constant<int, 64>());
