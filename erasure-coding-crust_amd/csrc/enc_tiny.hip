@@ -45,20 +45,23 @@ struct TinyArgs {
 };
 
 // the code's multiply tables, mslot[0 .. n-2] (every skew of IFFT_k at 0 and
-// FFT_k at the cosets below n), in the kernel arguments too
+// FFT_k at the cosets below n), in the kernel arguments too; NT - 1 slots
+// (NT = 8 for n <= 8, the reference benchmark's n_validators = 6: 560 B of
+// arguments instead of 1,200 B to copy per launch)
+template <int NT>
 struct TinyTabs {
-  MulTab t[kTinyMaxN - 1];
+  MulTab t[NT - 1];
 };
 
-template <int PB>
-__global__ void __launch_bounds__(kThreads) encode_tiny(TinyArgs<PB> pay, TinyTabs tt, uint32_t nv, uint32_t n,
+template <int PB, int NT>
+__global__ void __launch_bounds__(kThreads) encode_tiny(TinyArgs<PB> pay, TinyTabs<NT> tt, uint32_t nv, uint32_t n,
                                                          uint32_t logk, uint32_t npieces,
                                                          uint8_t *__restrict__ out, uint64_t ostride,
                                                          uint32_t *sig_flag, uint32_t sig_v) {
   const uint32_t tid = threadIdx.x, k = 1u << logk;
   // the tables into LDS in one parallel round of loads from the arguments
   // (read where used instead, each multiply waited for its own load)
-  __shared__ MulTab tabs[kTinyMaxN - 1];
+  __shared__ MulTab tabs[NT - 1];
   for (uint32_t i = tid; i < 5 * (n - 1); i += blockDim.x)  // (75 chunks at n = 16: more than a wave)
     reinterpret_cast<uint4 *>(tabs)[i] = reinterpret_cast<const uint4 *>(tt.t)[i];
   // piece p = symbols p*k .. p*k + k - 1, BE (poly_encoder.hpp:53-76):
@@ -186,11 +189,12 @@ bool tiny_applicable(const CodeParams &p, size_t plen, size_t ostride) {
 
 namespace {
 // the code's tables, built once per n on the host (mslot[i] = mtab[skews[i]])
-const TinyTabs &tiny_tabs(uint32_t n) {
-  static const std::array<TinyTabs, 5> all = [] {
-    std::array<TinyTabs, 5> a{};
+template <int NT>
+const TinyTabs<NT> &tiny_tabs(uint32_t n) {
+  static const std::array<TinyTabs<NT>, 5> all = [] {
+    std::array<TinyTabs<NT>, 5> a{};
     const Field &f = field();
-    for (int lg = 0; lg < 5; ++lg)
+    for (int lg = 0; lg < 5 && (1 << lg) <= NT; ++lg)
       for (uint32_t i = 0; i + 1 < (1u << lg); ++i) a[lg].t[i] = f.mtab[f.skews[i]];
     return a;
   }();
@@ -203,21 +207,25 @@ hipError_t launch_encode_tiny(const CodeParams &p, const DevTables &t, const uin
   if (!tiny_applicable(p, plen, ostride) || !out || !h_payload) return hipErrorInvalidValue;
   const uint32_t logk = uint32_t(__builtin_ctz(p.k));
   const uint32_t npieces = uint32_t(shard_len(p.k, plen) / 2);
-  const TinyTabs &tt = tiny_tabs(p.n);
-  const auto go = [&](auto tag) {
-    constexpr int PB = decltype(tag)::value;
+  const auto go = [&](auto tag, auto ntag) {
+    constexpr int PB = decltype(tag)::value, NT = decltype(ntag)::value;
     TinyArgs<PB> pay;
     // zero past the payload: the last piece's padding and the words a load
     // may read beyond it (clamped to the block)
     const size_t pad_end = std::min(size_t(PB), size_t(2) * p.k * npieces + 8);
     std::memcpy(pay.w, h_payload, plen);
     if (pad_end > plen) std::memset(reinterpret_cast<uint8_t *>(pay.w) + plen, 0, pad_end - plen);
-    hipLaunchKernelGGL(encode_tiny<PB>, dim3(1), dim3(block_for(npieces)), 0, s, pay, tt, p.nv, p.n, logk, npieces, out,
-                       uint64_t(ostride), sig ? sig->flag : nullptr, sig ? sig->v : 0u);
+    hipLaunchKernelGGL((encode_tiny<PB, NT>), dim3(1), dim3(block_for(npieces)), 0, s, pay, tiny_tabs<NT>(p.n),
+                       p.nv, p.n, logk, npieces, out, uint64_t(ostride), sig ? sig->flag : nullptr,
+                       sig ? sig->v : 0u);
   };
-  if (plen <= 64) go(std::integral_constant<int, 64>());
-  else if (plen <= 512) go(std::integral_constant<int, 512>());
-  else go(std::integral_constant<int, int(kTinyBytes)>());
+  const auto by_n = [&](auto tag) {
+    if (p.n <= 8) go(tag, std::integral_constant<int, 8>());
+    else go(tag, std::integral_constant<int, kTinyMaxN>());
+  };
+  if (plen <= 64) by_n(std::integral_constant<int, 64>());
+  else if (plen <= 512) by_n(std::integral_constant<int, 512>());
+  else by_n(std::integral_constant<int, int(kTinyBytes)>());
   const hipError_t e = hipGetLastError();
   if (e == hipSuccess && sig && sig->flag) sig->fused = true;
   return e;
@@ -253,16 +261,20 @@ hipError_t launch_systematic_tiny(const CodeParams &p, const uint8_t *h_shards, 
 // ECCR_Test_MeasurePerformance encode 546 us, the next ones 8-9 us), so the
 // device set-up pays it instead of the first call
 hipError_t warm_encode_tiny(hipStream_t s) {
-  const auto go = [&](auto tag) {
-    constexpr int PB = decltype(tag)::value;
+  const auto go = [&](auto tag, auto ntag) {
+    constexpr int PB = decltype(tag)::value, NT = decltype(ntag)::value;
     TinyArgs<PB> pay;
     pay.w[0] = 0;
-    hipLaunchKernelGGL(encode_tiny<PB>, dim3(1), dim3(kThreads), 0, s, pay, tiny_tabs(2), 2u, 2u, 0u, 0u, nullptr,
-                       uint64_t(0), nullptr, 0u);
+    hipLaunchKernelGGL((encode_tiny<PB, NT>), dim3(1), dim3(kThreads), 0, s, pay, tiny_tabs<NT>(2), 2u, 2u, 0u, 0u,
+                       nullptr, uint64_t(0), nullptr, 0u);
   };
-  go(std::integral_constant<int, 64>());
-  go(std::integral_constant<int, 512>());
-  go(std::integral_constant<int, int(kTinyBytes)>());
+  const auto both = [&](auto tag) {
+    go(tag, std::integral_constant<int, 8>());
+    go(tag, std::integral_constant<int, kTinyMaxN>());
+  };
+  both(std::integral_constant<int, 64>());
+  both(std::integral_constant<int, 512>());
+  both(std::integral_constant<int, int(kTinyBytes)>());
   const auto gs = [&](auto tag) {
     constexpr int PB = decltype(tag)::value;
     TinyArgs<PB> a;
