@@ -16,6 +16,16 @@ __global__ void __launch_bounds__(256) k(uint32_t *out, int iters, uint32_t c0) 
       if (OP == 3) x[i] = (x[i] >> 3) & 0x07070707u;                          // shr + and
       if (OP == 4) x[i] = __builtin_amdgcn_perm(x[i], z, y);                  // perm, table dep
       if (OP == 5) x[i] = x[i] * 0x9E3779B1u + y;                             // v_mad_u32_u24? (mul_lo)
+      if (OP == 6) {                                                           // v_lshrrev_b64 (pairs)
+        if (i % 2 == 0) {
+          uint64_t v = (uint64_t(x[i + 1]) << 32) | x[i];
+          asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(v));
+          x[i] = uint32_t(v);
+          x[i + 1] = uint32_t(v >> 32);
+        }
+      }
+      if (OP == 7) x[i] = __builtin_amdgcn_alignbit(x[i], y, 3);              // v_alignbit_b32
+      if (OP == 8) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(x[i]));     // v_lshrrev_b32 alone
     }
   }
   uint32_t r = 0;
@@ -23,7 +33,7 @@ __global__ void __launch_bounds__(256) k(uint32_t *out, int iters, uint32_t c0) 
   out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
 template <int OP>
-void run(const char *name, uint32_t *out, int ninstr_per_iter) {
+void run(const char *name, uint32_t *out, double ninstr_per_iter) {
   const int blocks = 4096, iters = 2000;
   hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
   hipLaunchKernelGGL(k<OP>, dim3(blocks), dim3(256), 0, 0, out, iters, 12345u);
@@ -39,5 +49,8 @@ int main() {
   uint32_t *out; hipMalloc(&out, 4096 * 256 * 4);
   run<0>("perm", out, 1); run<1>("bitop3", out, 1); run<2>("xor", out, 1);
   run<3>("shr+and", out, 2); run<4>("perm-tab", out, 1); run<5>("mul+add", out, 2);
+  // round 5: the 64-bit selector shift of mul_acc against 32-bit forms (the
+  // b64 run issues CH / 2 instructions per iteration)
+  run<6>("shr_b64", out, 0.5); run<7>("alignbit", out, 1); run<8>("shr_b32", out, 1);
   return 0;
 }
