@@ -17,12 +17,21 @@ CSRC = os.path.join(ROOT, "erasure-coding-crust_amd", "csrc")
 HIPCC = "/opt/rocm/bin/hipcc"
 
 
+def _sched_flags(name):
+    """The per-source scheduler flags of the library build (Makefile
+    `SCHED_<source> ?= ...`), so the checked code is the shipped code."""
+    mk = open(os.path.join(ROOT, "erasure-coding-crust_amd", "Makefile")).read()
+    m = re.search(r"^SCHED_" + re.escape(name) + r"\s*\??=\s*(.*)$", mk, re.M)
+    return m.group(1).split() if m else []
+
+
 def _asm(name, tmp_path):
     if not os.path.exists(HIPCC):
         pytest.skip("no hipcc")
     out = tmp_path / (name + ".s")
     subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
-                    "-o", str(out), os.path.join(CSRC, name)], check=True, capture_output=True)
+                    *_sched_flags(name), "-o", str(out), os.path.join(CSRC, name)], check=True,
+                   capture_output=True)
     return out.read_text()
 
 
@@ -43,6 +52,11 @@ def _nt_store_blocks(text, kernel):
         if re.match(r"\s+global_store_dwordx4 .* nt\b", l):
             cur += 1
     return counts
+
+
+def test_sched_flags_parsed():
+    assert _sched_flags("enc_k256w.hip") == ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]
+    assert _sched_flags("dec_n1024x.hip") == []
 
 
 def test_enc_k1024_fast_store_count(tmp_path):
