@@ -164,8 +164,16 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
     // the pattern's locator: computed once per device, then reused (§8f row 3)
     std::shared_ptr<const Locator> loc = cached_locator(d, p, present, c->stream);
     if (!loc) return false;
+    // on every path below `loc` is dropped only after the stream finished (the
+    // cache recycles entries nobody holds, and uses an entry's event only
+    // while it is not done: ec_runtime.hpp)
+    const auto release = [&](bool ok) {
+      if (!ok) (void)hipStreamSynchronize(c->stream);
+      locator_done(d, *loc);
+      return ok;
+    };
     ScratchLease lease(d, reconstruct_scratch_bytes(p, sl, 1), c->stream);
-    if (!lease.ok()) return false;
+    if (!lease.ok()) return release(false);
     void *scratch = lease.ptr();
     const bool launched = hip_check(launch_reconstruct(p, device_tables(d), src, sl, dstride,
                                                        loc->d_present, loc->d_elog, nullptr, 1,
@@ -174,13 +182,13 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
     const bool copied = launched && (direct || hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes,
                                                                         hipMemcpyDeviceToHost, c->stream),
                                                          "D2H"));
-    // `loc` is released only after the stream has finished with it (on every
-    // path: the locator cache recycles entries nobody holds).  Kernels only
-    // (direct): the signal-kernel wait; after a D2H copy the copy-to-kernel
-    // hand-off makes that slower than waiting on the stream
-    const bool synced = direct ? finish_call(c, "reconstruct", &sig)
-                               : hip_check(hipStreamSynchronize(c->stream), "reconstruct");
-    return launched && copied && synced;
+    // Kernels only (direct): the signal-kernel wait; after a D2H copy the
+    // copy-to-kernel hand-off makes that slower than waiting on the stream
+    // 
+    const bool synced = (launched && copied) &&
+                        (direct ? finish_call(c, "reconstruct", &sig)
+                                : hip_check(hipStreamSynchronize(c->stream), "reconstruct"));
+    return release(launched && copied && synced);
   }
   return (direct || hip_check(hipMemcpyAsync(c->h_out, c->d_out, out_bytes, hipMemcpyDeviceToHost,
                                              c->stream),

@@ -31,6 +31,7 @@ struct DeviceState {
   void *scratch = nullptr;
   size_t scratch_cap = 0;
   hipEvent_t scratch_done = nullptr;  // the last lease's work on its stream
+  hipStream_t scratch_stream = nullptr;  // that stream (a HostCtx's)
   bool scratch_used = false;
   std::mutex loc_mu;
   std::list<std::shared_ptr<Locator>> loc;  // most recent first
@@ -301,14 +302,33 @@ ScratchLease::~ScratchLease() {
   if (!held_) return;
   if (!d_->scratch_done) (void)hipEventCreateWithFlags(&d_->scratch_done, hipEventDisableTiming);
   d_->scratch_used = d_->scratch_done && hipEventRecord(d_->scratch_done, s_) == hipSuccess;
+  d_->scratch_stream = s_;
   d_->scratch_mu.unlock();
 }
 
-Locator::~Locator() {
-  if (ready) {
-    (void)hipEventSynchronize(ready);  // no copy / kernel still uses the buffers
-    (void)hipEventDestroy(ready);
+namespace {
+// A HostCtx's stream, synchronised, is about to be destroyed: the scratch
+// event recorded on it is complete and must not be waited on any more (HIP
+// would consult the destroyed stream).  Locator events need nothing: their
+// creating call marks them done before it returns (locator_done).
+void forget_stream(int dev, hipStream_t s) {
+  DeviceState *d = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (dev >= 0 && size_t(dev) < g_dev.size()) d = g_dev[dev].get();
   }
+  if (!d) return;
+  std::lock_guard<std::mutex> lk(d->scratch_mu);
+  if (d->scratch_stream == s) {
+    d->scratch_used = false;
+    d->scratch_stream = nullptr;
+  }
+}
+}  // namespace
+
+Locator::~Locator() {
+  // idle: every holder synchronised its stream before dropping it
+  if (ready) (void)hipEventDestroy(ready);
   if (d_present) (void)hipFree(d_present);
   if (d_elog) (void)hipFree(d_elog);
 }
@@ -328,7 +348,9 @@ std::shared_ptr<const Locator> cached_locator(DeviceState *d, const CodeParams &
         d->loc.erase(it);
         d->loc.push_front(hit);
         ++d->loc_hits;
-        if (!hip_ok(hipStreamWaitEvent(stream, hit->ready, 0), "locator wait")) return nullptr;
+        // not done: the creating call is still in flight (it marks the entry
+        // under this lock before returning), so `ready`'s stream is alive
+        if (!hit->done && !hip_ok(hipStreamWaitEvent(stream, hit->ready, 0), "locator wait")) return nullptr;
         return hit;
       }
     ++d->loc_misses;
@@ -343,9 +365,13 @@ std::shared_ptr<const Locator> cached_locator(DeviceState *d, const CodeParams &
   const uint16_t *fold = device_fold(d, p.n);
   if (!fold) return nullptr;
   if (L) {
-    // its kernel (and the H2D of its key) finished long ago in practice; wait
-    // on the host, as the key below is rewritten by the host
-    if (!hip_ok(hipEventSynchronize(L->ready), "locator recycle wait")) return nullptr;
+    // nobody holds it, so every call that used it has synchronised its stream
+    // (its kernel and the H2D of its key are complete); a fresh event, as the
+    // old one may belong to a destroyed stream
+    (void)hipEventDestroy(L->ready);
+    L->ready = nullptr;
+    L->done = false;
+    if (!hip_ok(hipEventCreateWithFlags(&L->ready, hipEventDisableTiming), "hipEventCreate")) return nullptr;
   } else {
     L = std::make_shared<Locator>();
     L->cap_n = p.n;
@@ -471,6 +497,11 @@ bool release_stream_scratch(DeviceState *d, hipStream_t s) {
   return true;
 }
 
+void locator_done(DeviceState *d, const Locator &L) {
+  std::lock_guard<std::mutex> lk(d->loc_mu);
+  L.done = true;
+}
+
 void locator_cache_stats(DeviceState *d, unsigned long *hits, unsigned long *misses) {
   std::lock_guard<std::mutex> lk(d->loc_mu);
   if (hits) *hits = d->loc_hits;
@@ -509,6 +540,7 @@ HostCtx::~HostCtx() {
                         hipSetDevice(device) == hipSuccess;
   if (stream) {
     (void)hipStreamSynchronize(stream);
+    forget_stream(device, stream);
     (void)hipStreamDestroy(stream);
   }
   for (uint8_t *h : {h_in, h_out})

@@ -100,18 +100,26 @@ struct Locator {
   std::vector<uint8_t> present;  // the key: [n] flags
   uint8_t *d_present = nullptr;  // [n] on the device
   uint16_t *d_elog = nullptr;    // [n] log-domain multipliers (ECCR_AMD_error_locator)
-  hipEvent_t ready = nullptr;    // recorded after the locator kernel
-  ~Locator();                    // waits for `ready`, then frees (never under the cache lock)
+  hipEvent_t ready = nullptr;    // recorded after the locator kernel, on the creating call's stream
+  mutable bool done = false;     // that kernel is known complete (under the cache lock)
+  ~Locator();                    // frees (never under the cache lock)
 };
 // The pattern's locator, computed on `stream` on a miss; on a hit `stream`
 // is ordered after the kernel that computed it.  nullptr on a HIP error.
-// Holders synchronise their stream before dropping the pointer (every C-ABI
-// call does), so an evicted entry nobody holds is idle apart from its own
-// locator kernel: a miss recycles its buffers and event (ordered after that
-// kernel) instead of freeing and allocating.
+// Every holder synchronises its stream before dropping the pointer, and the
+// creating call then marks the entry done (locator_done), so an entry nobody
+// holds is idle: a miss recycles its buffers instead of freeing and
+// allocating.  `ready` is used only while the entry is not done, i.e. while
+// the creating call (and so its thread's stream) is still alive: an event
+// whose recording stream was destroyed with its thread is never synchronised
+// on (HIP then read the stale stream: "operation not permitted on an event
+// last recorded in a capturing stream", round 5).
 std::shared_ptr<const Locator> cached_locator(DeviceState *d, const CodeParams &p,
                                               const std::vector<uint8_t> &present,
                                               hipStream_t stream);
+// The creating (or any) call's stream has finished everything issued after
+// the entry's locator kernel: later hits need no event wait.
+void locator_done(DeviceState *d, const Locator &L);
 void locator_cache_stats(DeviceState *d, unsigned long *hits, unsigned long *misses);
 
 // Growable buffers of one host thread (reentrancy = the reference's

@@ -174,6 +174,9 @@ def _batch_case(nv, plen, batch, cnt_key="threshold", seed0=0, pad=0):
     (6, 300, 5, 0), (1024, 5000, 3, 0), (1024, 70000, 2, 0), (4096, 3001, 2, 0), (100, 1, 4, 0),
     (1024, 5000, 3, 64), (1024, 70000, 2, 16), (1024, 1, 3, 16), (1024, 511, 2, 8),
     (1024, 131073, 2, 64), (1000, 99999, 2, 64), (800, 12345, 3, 64), (4096, 3001, 2, 64),
+    # k = 256 / n = 1024 encode: 9, 9 (last one partial), 8 and 7 groups of 8
+    # pieces per payload (one full tile plus a partial one, one tile, a partial one)
+    (1024, 36864, 4, 0), (900, 36000, 5, 16), (1024, 30000, 5, 64), (800, 28000, 3, 64),
     # k = 1024 / n = 4096 fast path (config 4): several 64-piece tiles, a partly
     # populated last coset (nv 3500), tight and 8/16/64-byte row pitches
     (4096, 300001, 2, 64), (3070, 300001, 2, 16), (3500, 131073, 2, 8), (4096, 131072, 1, 0),
@@ -1005,6 +1008,41 @@ def test_scratch_failure_is_reported(oracle):
     finally:
         E.set_scratch_limit(0)
     assert E.obtain_chunks(nv, p) == oracle.encode(nv, p)
+
+
+def test_locator_and_scratch_after_thread_exit(oracle):
+    """Locator-cache entries and the per-call scratch are used by short-lived
+    threads, whose streams are destroyed at exit; later calls on other threads
+    hit, evict and recycle those entries and lease the scratch again (round 5:
+    an event recorded on a destroyed stream was synchronised on and HIP
+    reported "operation not permitted on an event last recorded in a
+    capturing stream")."""
+    import threading
+    nv, plen = 1024, 3000
+    n, k, thr = E.code_params(nv)
+    p = synth.payload(7, plen).tobytes()
+    sh = E.obtain_chunks(nv, p)
+    sets = [set(int(x) for x in synth.present_set(70_000 + j, nv, thr)) for j in range(72)]
+    errs = []
+
+    def run(js):
+        try:
+            for j in js:
+                assert decode_subset(nv, sh, sets[j])[:plen] == p, j
+        except Exception as e:  # reported by the main thread
+            errs.append(e)
+
+    for t0 in range(0, 24, 4):  # 6 threads x 4 patterns, each thread gone before the next
+        t = threading.Thread(target=run, args=(range(t0, t0 + 4),))
+        t.start()
+        t.join()
+    assert not errs, errs
+    run([0, 5, 23])  # hits on entries created by exited threads
+    run(range(24, 72))  # misses: recycle the least recent entries (the exited threads')
+    run(range(0, 8))  # evicted by now: misses again
+    assert not errs, errs
+    keep = sets[3]
+    assert decode_subset(nv, sh, keep) == oracle.reconstruct(nv, [sh[i] if i in keep else None for i in range(nv)])
 
 
 def test_thread_exit_releases_contexts():
