@@ -339,6 +339,168 @@ def size_sweep(args, nv, cnt_key, dev, stream, dist, world, rank, backend, headl
     return rows
 
 
+def pcie_bandwidth(dev, nbytes=256 << 20, reps=4):
+    """Measured pinned-host <-> device copy rates on this box (the PCIe bound of
+    the host-resident path): H2D alone, D2H alone, and both at once on two
+    streams (aggregate bytes / time), GB/s."""
+    h_in = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True).fill_(1)
+    h_out = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d_a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    d_b = torch.ones(nbytes, dtype=torch.uint8, device=dev)
+    s_h2d, s_d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / reps
+
+    def duplex():
+        with torch.cuda.stream(s_h2d):
+            d_a.copy_(h_in, non_blocking=True)
+        with torch.cuda.stream(s_d2h):
+            h_out.copy_(d_b, non_blocking=True)
+
+    t_h2d = timed(lambda: d_a.copy_(h_in, non_blocking=True))
+    t_d2h = timed(lambda: h_out.copy_(d_b, non_blocking=True))
+    t_dup = timed(duplex)
+    del h_in, h_out, d_a, d_b
+    torch.cuda.empty_cache()
+    return {"h2d_GBps": round(nbytes / t_h2d / 1e9, 2), "d2h_GBps": round(nbytes / t_d2h / 1e9, 2),
+            "duplex_GBps": round(2 * nbytes / t_dup / 1e9, 2), "bytes_per_copy": nbytes}
+
+
+def _pcie_bound_s(pcie, h2d, d2h):
+    """Least time the copies of a host-resident call can take on this box: PCIe
+    is full duplex, so each direction at its own measured rate, at the same
+    time.  (`duplex_GBps`, two torch copies on two streams, is reported beside
+    it: on these boxes it has read as one direction's rate, i.e. those copies
+    did not overlap, while the library's pipeline does overlap them.)"""
+    return max(h2d / (pcie["h2d_GBps"] * 1e9), d2h / (pcie["d2h_GBps"] * 1e9))
+
+
+def _host_class(nv, plen, ids, dev):
+    """Pinned inputs of one payload-size class for the host-batch calls: the
+    payloads, their shard buffer, the compacted threshold-many present shards
+    (and their indices) of each, and the output buffer."""
+    n, k, thr = E.code_params(nv)
+    B, sl = len(ids), E.shard_len(nv, plen)
+    pay = torch.empty((B, plen), dtype=torch.uint8, pin_memory=True)
+    for c0 in range(0, B, 64):
+        pay[c0:c0 + 64] = synth.payloads_torch(ids[c0:c0 + 64], plen, device=dev).cpu()
+    sh = torch.empty((B, nv, sl), dtype=torch.uint8, pin_memory=True)
+    E.encode_host_batch(nv, pay, plen, plen, B, sh, sl, 0)
+    idx = np.stack([synth.present_set(10**6 + i, nv, thr) for i in ids]).astype(np.uint16)
+    comp = torch.empty((B, thr, sl), dtype=torch.uint8, pin_memory=True)
+    shn = sh.numpy()
+    for b in range(B):
+        comp[b] = torch.from_numpy(shn[b][idx[b].astype(np.int64)])
+    idx_t = torch.from_numpy(idx.view(np.int16)).pin_memory()
+    out = torch.empty((B, sl * k), dtype=torch.uint8, pin_memory=True)
+    return {"plen": plen, "B": B, "sl": sl, "pay": pay, "sh": sh, "comp": comp, "idx": idx_t,
+            "out": out}
+
+
+def e2e(args, nv, dev, dist, world, rank, cdev):
+    """north_star: "this path starts and ends in host memory ... the rate
+    including the H2D/D2H copies must also be measured".  Through the
+    host-batch pipeline (ECCR_AMD_encode_host_batch / _reconstruct_host_batch,
+    csrc/host_pipeline.hip; reference: erasure_coding.rs:246-264,404-406 take
+    and return host buffers), on every rank at once, max-over-ranks time:
+      config 2 shape: B x 1 MB pinned payloads -> H2D -> encode -> D2H of every
+        shard; then H2D of threshold-many compacted shards per payload ->
+        locator + reconstruct -> D2H of the payload;
+      config 5: the README size mix (15 B .. 10 MB, `--e2e-per-size` of each,
+        byte-balanced over the ranks), the same two calls per size class.
+    Each next to the PCIe bound from this box's measured pinned copy rates
+    (H2D and D2H at their own rates, at once).
+    Never the bench `value` (that one is device-resident)."""
+    n, k, thr = E.code_params(nv)
+    pcie = pcie_bandwidth(dev)
+
+    def timed(fn, reps):
+        fn()  # warm: pipeline slots, first touch
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        el = time.perf_counter() - t0
+        if dist:
+            dist.barrier()
+        return sharding.max_over_ranks(el / reps, dist, cdev)
+
+    def enc(c):
+        E.encode_host_batch(nv, c["pay"], c["plen"], c["plen"], c["B"], c["sh"], c["sl"], 0)
+
+    def rec(c):
+        E.reconstruct_host_batch(nv, c["comp"], c["sl"], c["sl"], c["idx"], thr, c["B"], c["out"],
+                                 c["sl"] * k, 0)
+
+    def moved(c):  # PCIe bytes of the encode and of the reconstruct call
+        B, plen, sl = c["B"], c["plen"], c["sl"]
+        return (B * plen, B * nv * sl), (B * thr * (sl + 2), B * sl * k)
+
+    # config 2 shape, a bounded batch per rank
+    c2 = _host_class(nv, args.payload, sharding.rank_seeds(rank, args.e2e_batch), dev)
+    t_e = timed(lambda: enc(c2), args.e2e_reps)
+    t_r = timed(lambda: rec(c2), args.e2e_reps)
+    (eh, ed), (rh, rd) = moved(c2)
+    be, br = _pcie_bound_s(pcie, eh, ed), _pcie_bound_s(pcie, rh, rd)
+    ok = bool(torch.equal(c2["out"][:, :args.payload], c2["pay"]))
+    gib = world * c2["B"] * args.payload / 2**30
+    cfg2 = {"payload_bytes": args.payload, "batch_per_gpu": c2["B"], "reps": args.e2e_reps,
+            "encode_GiBps": round(gib / t_e, 3), "reconstruct_GiBps": round(gib / t_r, 3),
+            "roundtrip_GiBps": round(gib / (t_e + t_r), 3),
+            "pcie_bound_roundtrip_GiBps": round(gib / (be + br), 3),
+            "frac_of_pcie_bound": round((be + br) / (t_e + t_r), 4),
+            "encode_frac_of_pcie_bound": round(be / t_e, 4),
+            "reconstruct_frac_of_pcie_bound": round(br / t_r, 4),
+            "pcie_bytes_per_gpu": {"encode_h2d": eh, "encode_d2h": ed, "reconstruct_h2d": rh,
+                                   "reconstruct_d2h": rd},
+            "roundtrip_ok": ok}
+    del c2
+    # config 5: the README size mix
+    sizes = [BENCH_SIZES[i % len(BENCH_SIZES)] for i in range(args.e2e_per_size * len(BENCH_SIZES))]
+    mine = sharding.balanced_partition(sizes, world)[rank]
+    by = {}
+    for i in mine:
+        by.setdefault(sizes[i], []).append(i)
+    work = [_host_class(nv, plen, ids, dev) for plen, ids in sorted(by.items())]
+
+    def one_pass():
+        for c in work:
+            enc(c)
+        for c in work:
+            rec(c)
+
+    t_m = timed(one_pass, args.e2e_reps)
+    bound = 0.0
+    for c in work:
+        (eh, ed), (rh, rd) = moved(c)
+        bound += _pcie_bound_s(pcie, eh, ed) + _pcie_bound_s(pcie, rh, rd)
+    bound = sharding.max_over_ranks(bound, dist, cdev)
+    ok5 = all(torch.equal(c["out"][:, :c["plen"]], c["pay"]) for c in work)
+    del work
+    total = sum(sizes)
+    cfg5 = {"sizes": list(BENCH_SIZES), "payloads": len(sizes), "stream_bytes": total,
+            "reps": args.e2e_reps, "roundtrip_GiBps": round(total / t_m / 2**30, 3),
+            "pcie_bound_roundtrip_GiBps": round(total / bound / 2**30, 3),
+            "frac_of_pcie_bound": round(bound / t_m, 4),
+            "partition": "sharding.balanced_partition (bytes, greedy LPT)", "roundtrip_ok": ok5}
+    if dist:
+        f = torch.tensor([int(ok and ok5)], dtype=torch.int32, device=cdev)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        ok = ok5 = bool(f.item())
+    return {"what": "host-resident path: pinned host -> H2D -> kernels -> D2H -> pinned host, "
+                    "whole job over all ranks, max-over-ranks time (not the bench value)",
+            "n_validators": nv, "present_shards": thr, "pcie_measured": pcie,
+            "config2": cfg2, "config5_mixed": cfg5}, ok and ok5
+
+
 def scatter_gather(dist, rank, world, dev, B, plen, d_pay, d_out, step_s, timeout_s,
                    on_timeout=None):
     """SURVEY.md §8e / north_star: the batch starts on GPU0 and the decoded
@@ -509,6 +671,13 @@ def main():
                     help="device shard row stride in bytes (0: shard_len rounded up to --row-align)")
     ap.add_argument("--row-align", type=int, default=64,
                     help="device shard row stride = shard_len rounded up to this many bytes")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the host-resident (PCIe-inclusive) `e2e` block")
+    ap.add_argument("--e2e-batch", type=int, default=256,
+                    help="1 MB-class payloads per GPU in the e2e config-2 leg")
+    ap.add_argument("--e2e-per-size", type=int, default=16,
+                    help="payloads of each README size in the e2e config-5 stream (whole job)")
+    ap.add_argument("--e2e-reps", type=int, default=3)
     ap.add_argument("--graph", action="store_true",
                     help="time K replays of one captured hipGraph step (ECCR_AMD_*_ws calls on "
                          "caller-owned scratch) instead of K eager steps")
@@ -694,6 +863,12 @@ def main():
         line["sizes"] = size_sweep(args, nv, args.present, dev, stream, dist, world, rank, backend,
                                    headline)
         ok = ok and all(r["roundtrip_ok"] for r in line["sizes"])
+    if not args.no_e2e:
+        del d_sh, d_el  # the host-batch pipeline allocates its own device slots
+        torch.cuda.empty_cache()
+        line["e2e"], ok_e2e = e2e(args, nv, dev, dist, world, rank,
+                                  dev if backend == "nccl" else torch.device("cpu"))
+        ok = ok and ok_e2e
     if backend != "nccl":
         line["rehearsal"] = f"{world} ranks on {line['n_gpus']} GPU(s), gloo"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # (contract: rank 0 at N = 1)

@@ -168,8 +168,11 @@ bool reconstruct_host(const CodeParams &p, const std::vector<uint8_t> &present, 
     // cache recycles entries nobody holds, and uses an entry's event only
     // while it is not done: ec_runtime.hpp)
     const auto release = [&](bool ok) {
-      if (!ok) (void)hipStreamSynchronize(c->stream);
-      locator_done(d, *loc);
+      // a failed synchronisation may mean the locator kernel itself faulted:
+      // the entry leaves the cache instead of being marked done, so no later
+      // hit skips the event wait and reads d_elog that was never written
+      if (!ok && hipStreamSynchronize(c->stream) != hipSuccess) locator_drop(d, *loc);
+      else locator_done(d, *loc);
       return ok;
     };
     ScratchLease lease(d, reconstruct_scratch_bytes(p, sl, 1), c->stream);
@@ -478,7 +481,12 @@ NPRSResult encode_batch(unsigned long nv, const uint8_t *d_payloads, unsigned lo
   if (sstride < shard_len(p.k, plen) || pstride < plen) return result(NPRS_RESULT_BAD_PAYLOAD);
   DeviceState *d = device_state();
   if (!d) return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
-  BatchScratch sc(d, encode_scratch_bytes(p, plen, batch), s, ws);
+  // a workspace below the queried size (e.g. a size of 0 cached from an older
+  // release) runs the shapes whose scratch is only a tile counter on the
+  // static schedule: slower, not an error
+  const bool optional = ws && (!ws->ptr || ws->bytes < encode_scratch_bytes(p, plen, batch)) &&
+                        encode_scratch_optional(p);
+  BatchScratch sc(d, optional ? 0 : encode_scratch_bytes(p, plen, batch), s, ws);
   if (!sc.ok) return result(NPRS_RESULT_UNKNOWN_CODE_PARAM);
   if (!hip_check(launch_encode(p, device_tables(d), d_payloads, plen, pstride, batch, d_shards,
                                sstride, sc.p, s),

@@ -84,15 +84,9 @@ __device__ __forceinline__ void tab_f9(uint32_t s, uint32_t c, F9Tab &T) {
 constexpr int tk(int k) { return k < 8 ? 0 : k < 12 ? 1 : k < 14 ? 2 : 3; }
 constexpr int bk(int k) { return k < 8 ? 2 * k : k < 12 ? 4 * (k - 8) : k < 14 ? 8 * (k - 12) : 0; }
 
-#ifndef N1024X_RV_EARLY
-#define N1024X_RV_EARLY 1
-#endif
-#ifndef N1024X_RA
-#define N1024X_RA 2
-#endif
-#ifndef N1024X_RB
-#define N1024X_RB 3
-#endif
+// table-ring depths of passes A and B (2 / 3: 2-2, 3-5 and 4-7 were within
+// noise, profiles/r05/NOTES.md; A/B variants: scripts/variants/n1024x_knobs.py)
+constexpr int RING_A = 2, RING_B = 3;
 
 // kind of a stage's table: 0 general, 1 F9, 2 subfield
 template <int B0, int T>
@@ -141,7 +135,7 @@ __device__ __forceinline__ void ipass_ring(S16 &s, Fetch &&fetch) {
 // is GF(2)-linear, so each address is a per-lane part XOR a compile-time one)
 __device__ __forceinline__ void ipassA(S16 &s, uint32_t lane) {
   const uint32_t ls = tlin(16 * lane), lc0 = tlin(8 * lane), lc1 = tlin(4 * lane) ^ tlin(512);
-  ipass_ring<0, N1024X_RA>(s, [&](int k, Tab &T) __attribute__((always_inline)) {
+  ipass_ring<0, RING_A>(s, [&](int k, Tab &T) __attribute__((always_inline)) {
     const int t = tk(k), blk = bk(k);
     const uint32_t a = ls ^ tlin(skew_idx(uint32_t(blk), t));
     if (t == 0) {
@@ -163,26 +157,12 @@ __device__ __forceinline__ void ipassA(S16 &s, uint32_t lane) {
 // IFFT pass B (position bits 4-7 in registers): subfield tables only
 __device__ __forceinline__ void ipassB(S16 &s, uint32_t lane) {
   const uint32_t lb = tlin((lane >> 4) << 8);
-  ipass_ring<4, N1024X_RB>(s, [&](int k, Tab &T) __attribute__((always_inline)) {
+  ipass_ring<4, RING_B>(s, [&](int k, Tab &T) __attribute__((always_inline)) {
     SubTab U;
     tab_at(nullptr, lb ^ tlin(skew_idx(uint32_t(bk(k)) << 4, 4 + tk(k))), U);
 #pragma unroll
     for (int i = 0; i < 5; ++i) T.t[i] = U.t[i];
   });
-}
-
-// issue priority by transform phase (experiments): waves w, w + 4, w + 8
-// share a SIMD; N1024X_PRIO = 1 lets group 2 (w >= 8) lead pass A, group 1
-// pass B, group 0 pass C and the FFT; 2 the reverse; 0 equal throughout
-#ifndef N1024X_PRIO
-#define N1024X_PRIO 0
-#endif
-__device__ __forceinline__ void prio3(uint32_t wave_s, int phase) {
-  if constexpr (N1024X_PRIO != 0) {
-    const uint32_t lead = N1024X_PRIO == 1 ? 2u - uint32_t(phase) : uint32_t(phase);
-    if (phase < 3 && (wave_s >> 2) == lead) __builtin_amdgcn_s_setprio(2);
-    else __builtin_amdgcn_s_setprio(0);
-  }
 }
 
 // bytes [0, avail) (avail < 96) of a 16-B aligned row slice into w[24], zero
@@ -342,8 +322,8 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
     // phase 5's received rows y = 4 lane + q < 256 (8 B of the row: this
     // group's 4 columns), re-read from the shards (L2: the gather has just
     // read them; no LDS left to stage them), requested before the IFFT
-    // (N1024X_RV_EARLY = 0: after it; A/B at B = 4096: 10.68 / 10.92 ms
-    // against 10.76 / 11.00, and 154 VGPRs instead of 168)
+    // (10.68 / 10.92 ms at B = 4096 with 154 VGPRs, against 10.76 / 11.00
+    // requested after it; profiles/r05/NOTES.md)
     uint2 rv[4];
     const auto load_rv = [&]() __attribute__((always_inline)) {
       uint32_t ol2 = lane;
@@ -359,7 +339,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
         }
       }
     };
-    if (N1024X_RV_EARLY) load_rv();
+    load_rv();
 
     S16 s;
     // ---- phase 2: IFFT_1024 on this wave's group
@@ -371,7 +351,6 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
         s.l[r] = x.x;
         s.h[r] = x.y;
       }
-      prio3(wave_s, 0);
       ipassA(s, lane);
 #pragma unroll
       for (int r = 0; r < 16; ++r) lds_st2(la ^ raddr(r), make_uint2(s.l[r], s.h[r]));
@@ -387,14 +366,12 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
         s.l[r] = x.x;
         s.h[r] = x.y;
       }
-      prio3(wave_s, 1);
       ipassB(s, lane);  // stages 4-7: subfield (planes 0, 1)
 #pragma unroll
       for (int r = 0; r < 16; ++r) lds_st2(lb ^ raddr(uint32_t(r) << 4), make_uint2(s.l[r], s.h[r]));
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
-    prio3(wave_s, 2);
     // layout C: r bit0 = p8, bit1 = p9, bit2 = p6, bit3 = p7; lane = p0..p5
     const uint32_t lc = lds_addr(my) | raddr(lane);
 #pragma unroll
@@ -433,7 +410,6 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
       // across the tile loop, and spilled, by the compiler)
       load_tab(t.mtab_tout, m != 0xFFFFu ? m : 0u, T5[q]);  // tower in, symbols out
     }
-    if (!N1024X_RV_EARLY) load_rv();
 
     // ---- phases 3 + 4: the closed-form derivative at y < 256 and the FFT
     // restricted to y < 256 (dec_n1024.hip, the same steps)
@@ -549,7 +525,6 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
       fb(2, 3, T[1]);
     }
 
-    prio3(wave_s, 3);
     // ---- phase 5: y = 4*lane + q; columns cbase + c (decode_main:185-188,
     // reconstructSub:138-149)
     {

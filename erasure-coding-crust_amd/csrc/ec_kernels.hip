@@ -558,6 +558,12 @@ hipError_t launch_signal_host(uint32_t *h_flag, uint32_t v, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Encode scratch that is only a tile counter (k = 256 / 512 / 1024 fast
+// kernels): optional, the kernels fall back to a static schedule without it.
+bool encode_scratch_optional(const CodeParams &p) {
+  return k1024_applicable(p) || k256_applicable(p) || encgen_applicable(p);
+}
+
 size_t encode_scratch_bytes(const CodeParams &p, size_t plen, size_t batch) {
   if (k1024_applicable(p)) return k1024_scratch_bytes(plen, batch);
   if (k256_applicable(p)) return k256_scratch_bytes(p);
@@ -583,7 +589,7 @@ hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t 
     return launch_encode_k256(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
   if (aligned && encgen_applicable(p))
     return launch_encode_gen(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
-  if (aligned && scratch && k1024_applicable(p))
+  if (aligned && k1024_applicable(p))
     return launch_encode_k1024(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
   const size_t sl = shard_len(p.k, plen);
   const int G = groups_for(p.k);

@@ -95,6 +95,7 @@ hipError_t prepare_kernel(const void *fn, int lds_bytes, int *cus);
 // Scratch (global memory) needed by each launch for FFT sizes whose working
 // set does not fit LDS; 0 for the common sizes.
 size_t encode_scratch_bytes(const CodeParams &p, size_t payload_len, size_t batch);
+bool encode_scratch_optional(const CodeParams &p);  // only a tile counter: static schedule without it
 size_t reconstruct_scratch_bytes(const CodeParams &p, size_t shard_len, size_t batch);
 
 hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,

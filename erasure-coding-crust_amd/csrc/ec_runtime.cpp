@@ -399,11 +399,18 @@ namespace {
 // Frees the evicted entries nobody holds any more, after a device
 // synchronisation (their streams may be gone, so the whole device is waited
 // for).  Called where waiting is allowed: never while `s` is being captured.
-void drain_dead(DeviceState *d, hipStream_t s) {
+// A device-wide synchronisation (and hipFree) made while ANOTHER thread
+// captures a stream in global mode invalidates that capture, so the implicit
+// drain at the start of a plain call runs only once kDeadDrain evicted buffers
+// have gathered (at most one such drain per kDeadDrain evictions, i.e. only
+// when more than 64 streams of a device use the plain calls; ec_amd.h); the
+// explicit one (ECCR_AMD_release_stream_scratch) always runs.
+constexpr size_t kDeadDrain = 16;
+void drain_dead(DeviceState *d, hipStream_t s, bool force) {
   std::list<std::shared_ptr<StreamScratchEntry>> dead;
   {
     std::lock_guard<std::mutex> lk(d->ss_mu);
-    if (d->ss_dead.empty()) return;
+    if (d->ss_dead.empty() || (!force && d->ss_dead.size() < kDeadDrain)) return;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
     for (auto it = d->ss_dead.begin(); it != d->ss_dead.end();)
@@ -423,7 +430,7 @@ void drain_dead(DeviceState *d, hipStream_t s) {
 
 StreamScratch::StreamScratch(DeviceState *d, hipStream_t s, size_t bytes) : want_(bytes) {
   if (!d || bytes == 0) return;
-  drain_dead(d, s);
+  drain_dead(d, s, false);
   const size_t limit = g_scratch_limit;
   if (limit && bytes > limit) {  // as if hipMalloc had failed
     set_error("erasure_coding_crust(amd): scratch of " + std::to_string(bytes) +
@@ -493,13 +500,24 @@ bool release_stream_scratch(DeviceState *d, hipStream_t s) {
     std::lock_guard<std::mutex> lk(d->ss_mu);
     d->ss_dead.push_back(std::move(e));
   }
-  drain_dead(d, s);
+  drain_dead(d, s, true);
   return true;
 }
 
 void locator_done(DeviceState *d, const Locator &L) {
   std::lock_guard<std::mutex> lk(d->loc_mu);
   L.done = true;
+}
+
+void locator_drop(DeviceState *d, const Locator &L) {
+  std::shared_ptr<Locator> gone;  // released after the lock (~Locator frees)
+  std::lock_guard<std::mutex> lk(d->loc_mu);
+  for (auto it = d->loc.begin(); it != d->loc.end(); ++it)
+    if (it->get() == &L) {
+      gone = std::move(*it);
+      d->loc.erase(it);
+      break;
+    }
 }
 
 void locator_cache_stats(DeviceState *d, unsigned long *hits, unsigned long *misses) {

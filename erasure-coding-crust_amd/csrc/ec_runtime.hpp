@@ -120,6 +120,9 @@ std::shared_ptr<const Locator> cached_locator(DeviceState *d, const CodeParams &
 // The creating (or any) call's stream has finished everything issued after
 // the entry's locator kernel: later hits need no event wait.
 void locator_done(DeviceState *d, const Locator &L);
+// The call that holds the entry failed to synchronise its stream (the locator
+// kernel may have faulted): the entry leaves the cache; its last holder frees it.
+void locator_drop(DeviceState *d, const Locator &L);
 void locator_cache_stats(DeviceState *d, unsigned long *hits, unsigned long *misses);
 
 // Growable buffers of one host thread (reentrancy = the reference's

@@ -158,7 +158,8 @@ __global__ void __launch_bounds__(THREADS)
   const uint32_t tid0 = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid0 >> 6);
   uint8_t *my = regions + wave * REG_BYTES;
   auto *slot = reinterpret_cast<__attribute__((address_space(3))) volatile uint32_t *>(uintptr_t(SLOT));
-  if (tid0 == 0) *slot = atomicAdd(tick, 1u);  // this workgroup's first tile
+  // this workgroup's first tile (no counter: a static grid stride)
+  if (tid0 == 0) *slot = tick ? atomicAdd(tick, 1u) : blockIdx.x;
   // cosets 1 .. ncos - 1 start below n_validators (poly_encoder.hpp:229-236)
   const uint32_t ncos = uint32_t(nv + K - 1) / K;
 
@@ -181,7 +182,7 @@ __global__ void __launch_bounds__(THREADS)
     const uint64_t b = cur / tiles_pp;
     const uint64_t piece0 = uint64_t(cur % tiles_pp) * TILE;
     uint32_t taken = 0;
-    if (tid0 == 0) taken = atomicAdd(tick, 1u);
+    if (tid0 == 0) taken = tick ? atomicAdd(tick, 1u) : cur + gridDim.x;
     uint8_t *SH = shards + b * uint64_t(nv) * sstride;
     const uint8_t *P = payloads + b * pstride;
     S16 g, coef;
@@ -267,9 +268,11 @@ hipError_t launch_encode_k1024(const CodeParams &p, const DevTables &t, const ui
   if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&encode_k1024_fused), LDS_BYTES, &cus);
       e != hipSuccess)
     return e;
-  if (!scratch || tiles >= (size_t(1) << 32) - size_t(2) * cus) return hipErrorInvalidValue;
+  if (tiles >= (size_t(1) << 32) - size_t(2) * cus) return hipErrorInvalidValue;
+  // the tile counter (k1024_scratch_bytes); none: the static schedule
   uint32_t *tick = static_cast<uint32_t *>(scratch);
-  if (const hipError_t e = launch_zero_counters(tick, sizeof(uint32_t), s); e != hipSuccess) return e;
+  if (tick)
+    if (const hipError_t e = launch_zero_counters(tick, sizeof(uint32_t), s); e != hipSuccess) return e;
   const unsigned grid = unsigned(std::min(tiles, size_t(cus)));
   hipLaunchKernelGGL(encode_k1024_fused, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads,
                      uint64_t(plen), uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride),

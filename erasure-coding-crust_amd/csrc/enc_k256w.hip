@@ -240,7 +240,9 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k256w(const uint8_t *__rest
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid0 = threadIdx.x;
   auto *slot = reinterpret_cast<__attribute__((address_space(3))) volatile uint32_t *>(uintptr_t(SLOT));
-  if (tid0 == 0) *slot = atomicAdd(tick, 1u);  // this workgroup's first tile
+  // this workgroup's first tile; without a counter (no scratch) a static
+  // grid stride (slower: the two workgroups of a CU drift apart, below)
+  if (tid0 == 0) *slot = tick ? atomicAdd(tick, 1u) : blockIdx.x;
   {  // the compact image (32 KB), every load issued before the first store
     constexpr int kPer = int(kCImgBytes / 16 / THREADS);
     v4u v[kPer];
@@ -326,7 +328,7 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k256w(const uint8_t *__rest
     xb.c = mswz(ulaneC(q, inst));
     const uint64_t b = cur / tiles_pp, piece0 = uint64_t(cur % tiles_pp) * TILE;
     uint32_t taken = 0;  // thread 0: the tile taken for after this one
-    if (tid0 == 0) taken = atomicAdd(tick, 1u);
+    if (tid0 == 0) taken = tick ? atomicAdd(tick, 1u) : cur + gridDim.x;
     uint32_t next = 0;   // every wave: that tile, read from the slot
     uint8_t *SH = shards + b * uint64_t(nv) * sstride;
     // the last coset of this n_validators (uniform), after whose staging the
@@ -460,10 +462,13 @@ hipError_t launch_encode_k256w(const CodeParams &p, const DevTables &t, const ui
   if (p.nv <= 2 * K || p.nv > 1024) return hipErrorInvalidValue;  // cosets 256, 512 (, 768)
   const size_t sl = shard_len(p.k, plen);
   const size_t tiles = (sl / 2 + TILE - 1) / TILE * batch;
-  if (!scratch || tiles >= (size_t(1) << 32) - size_t(4) * cus) return hipErrorInvalidValue;
-  // the tile counter (k256w_scratch_bytes), zeroed in stream order
+  if (tiles >= (size_t(1) << 32) - size_t(4) * cus) return hipErrorInvalidValue;
+  // the tile counter (k256_scratch_bytes), zeroed in stream order; no
+  // scratch: the static schedule (a missing counter costs speed,
+  // not an error)
   uint32_t *tick = static_cast<uint32_t *>(scratch);
-  if (const hipError_t e = launch_zero_counters(tick, sizeof(uint32_t), s); e != hipSuccess) return e;
+  if (tick)
+    if (const hipError_t e = launch_zero_counters(tick, sizeof(uint32_t), s); e != hipSuccess) return e;
   const size_t slots = 2 * size_t(cus);  // two workgroups per CU
   const unsigned grid = unsigned(tiles < slots ? tiles : slots);
   hipLaunchKernelGGL(encode_k256w, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads, uint64_t(plen),

@@ -10,7 +10,7 @@
 //    host-side copy into the staging buffer);
 //  * so do the code's skew tables (n - 1 <= 15 of them, mslot[0 .. n-2],
 //    built on the host): no dependent device-memory round trip, no LDS;
-//  * one thread per piece keeps its k <= 8 symbols in registers through the
+//  * one thread per piece keeps its k <= 4 symbols (kMaxK; tiny_applicable: n <= 16) in registers through the
 //    IFFT_k and each coset's FFT_k (additive_fft.hpp:99-141; encodeLow,
 //    poly_encoder.hpp:217-240), and writes its 2-byte BE symbol of every shard
 //    row straight to the pinned output (a wave's 64 pieces are 128 contiguous

@@ -18,8 +18,15 @@
  * all its kernels, so the calls run one after the other on the stream.  A
  * stream keeps its largest scratch until ECCR_AMD_release_stream_scratch or
  * until more than 64 streams of the device have one: then the least recently
- * used is released after a device-wide synchronisation (which waits for work
- * on every stream of the device).  The *_ws variants take caller-owned scratch instead (size from
+ * used is evicted, and evicted buffers are freed 16 at a time, after a
+ * device-wide synchronisation (which waits for work on every stream of the
+ * device), at the start of a plain call on a stream that is not being
+ * captured.  That synchronisation invalidates a hipGraph capture another
+ * thread has open in global mode (hipStreamCaptureModeGlobal) at that moment:
+ * programs that capture in global mode while more than 64 streams use the
+ * plain calls should release retired streams' scratch with
+ * ECCR_AMD_release_stream_scratch (outside any capture), use the *_ws calls,
+ * or capture in thread-local / relaxed mode.  The *_ws variants take caller-owned scratch instead (size from
  * the matching *_workspace_bytes query) and never allocate.  Either form can
  * be captured into a hipGraph and replayed once the shape has run once on the
  * stream outside capture (the first call per (device, kernel) also sets a
@@ -91,7 +98,11 @@ struct NPRSResult ECCR_AMD_reconstruct_batch(unsigned long n_validators, const u
  * also 0 for invalid parameters, which the calls themselves report), and the
  * same calls with that scratch passed in: d_workspace 256-B aligned, at least
  * the queried size (else UNKNOWN_* and nothing is launched).  A workspace may
- * be shared by calls that are ordered on one stream. */
+ * be shared by calls that are ordered on one stream.  Encode shapes with
+ * k = 16 .. 1024 and n <= 4096 (n_validators 46 .. 4096) query 256 bytes
+ * since round 5: a tile counter for their dynamic schedule.  A smaller (or NULL) workspace is accepted for those
+ * shapes and runs them on a static schedule (a few percent slower), so a size
+ * of 0 cached from an earlier release still works. */
 unsigned long ECCR_AMD_encode_workspace_bytes(unsigned long n_validators,
                                               unsigned long payload_len, unsigned long batch);
 unsigned long ECCR_AMD_error_locator_workspace_bytes(unsigned long n_validators,

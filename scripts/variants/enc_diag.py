@@ -6,6 +6,13 @@ that work costs in the real interleaving:
 
   enc_diag.py KIND OUTDIR   writes OUTDIR/enc_k256w.hip and OUTDIR/cimg.hpp
     nobar   the per-tile workgroup barriers dropped (LDS races: garbage rows)
+    static  tiles by a static grid stride instead of the ticket counter: with
+            barriers dropped the tickets are read unsynchronised (lagging
+            waves skip or repeat tiles), so combine nobar / cmp with static
+            for a time account (nobar+static, cmp+static)
+    nbread  only the "regions read out" barriers dropped (tile start, after
+            IFFT pass A, before each coset's first exchange)
+    nbstg   only the "rows staged" barriers dropped (before each store phase)
     nost    the row stores dropped (LDS reads kept; nothing written)
     nold    payload loads replaced by lane-derived words
     nostg   row stores dropped, their LDS reads and addresses kept (asm-consumed)
@@ -79,6 +86,22 @@ for k in kinds:
     if k == "nobar":
         enc = rep(enc, "const auto rsync = [&]() __attribute__((always_inline)) { lds_barrier(); };",
                   "const auto rsync = [&]() __attribute__((always_inline)) { asm volatile(\"\" ::: \"memory\"); };")
+    elif k == "static":
+        enc = rep(enc, "  uint32_t cur = __builtin_amdgcn_readfirstlane(*slot);", "  uint32_t cur = blockIdx.x;")
+        enc = rep(enc, "      next = __builtin_amdgcn_readfirstlane(*slot);", "      next = cur + gridDim.x;")
+    elif k == "nbread":
+        for old in ("    rsync();  // the other waves are done reading this region (last tile)\n",
+                    "    rsync();  // systematic rows read out of the regions\n",
+                    "      rsync();  // previous coset's rows read out\n",
+                    "      rsync();  // tile start\n", "      rsync();  // after IFFT pass A\n",
+                    "        rsync();  // after pass C\n"):
+            enc = rep(enc, old, "")
+    elif k == "nbstg":
+        for old, new in (("    rsync();\n    store_sys();", "    store_sys();"),
+                         ("      rsync();\n      if constexpr (decltype(last)::value)", "      if constexpr (decltype(last)::value)"),
+                         ("      rsync();  // systematic rows staged\n", ""),
+                         ("        rsync();  // rows staged\n", "")):
+            enc = rep(enc, old, new)
     elif k == "nost":
         enc = rep(enc, "  asm volatile(\"\" : \"+v\"(lane));  // recomputed here, not kept live across the FFTs\n",
                   "  asm volatile(\"\" : \"+v\"(lane));\n  if (s0 != 0xFFFFFFFFu) {\n    then();\n    return;\n  }\n")

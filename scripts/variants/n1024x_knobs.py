@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""A/B variants of reconstruct_n1024x's tuning choices (moved out of the
+product source; results in profiles/r05/NOTES.md):
+
+  n1024x_knobs.py KNOB=VALUE[,KNOB=VALUE...] OUT.hip
+    RA=N, RB=N   table-ring depth of IFFT pass A / pass B (product: 2 / 3)
+    RVLATE=1     phase 5's re-reads requested after IFFT pass C instead of
+                 before the IFFT (product: before)
+    PRIO=1|2     issue priority by transform phase: 1 lets waves 8-11 lead
+                 pass A, 4-7 pass B, 0-3 pass C and the FFT; 2 the reverse
+                 (product: equal priority)
+
+Build: scripts/build_var.sh NAME "" dec_n1024x.hip=OUT.hip"""
+import sys
+
+ROOT = __file__.rsplit("/scripts/", 1)[0]
+knobs = dict(kv.split("=") for kv in sys.argv[1].split(",") if kv)
+out = sys.argv[2]
+s = open(f"{ROOT}/erasure-coding-crust_amd/csrc/dec_n1024x.hip").read()
+
+
+def rep(s, old, new):
+    assert old in s, old[:80]
+    return s.replace(old, new, 1)
+
+
+if "RA" in knobs or "RB" in knobs:
+    s = rep(s, "constexpr int RING_A = 2, RING_B = 3;",
+            f"constexpr int RING_A = {knobs.get('RA', 2)}, RING_B = {knobs.get('RB', 3)};")
+if knobs.get("RVLATE") == "1":
+    s = rep(s, "    load_rv();\n\n    S16 s;", "\n    S16 s;")
+    s = rep(s, "    // ---- phases 3 + 4:", "    load_rv();\n\n    // ---- phases 3 + 4:")
+if knobs.get("PRIO") in ("1", "2"):
+    lead = "2u - uint32_t(phase)" if knobs["PRIO"] == "1" else "uint32_t(phase)"
+    s = rep(s, "}  // namespace\n\n__global__",
+            "__device__ __forceinline__ void prio3(uint32_t wave_s, int phase) {\n"
+            f"  const uint32_t lead = {lead};\n"
+            "  if (phase < 3 && (wave_s >> 2) == lead) __builtin_amdgcn_s_setprio(2);\n"
+            "  else __builtin_amdgcn_s_setprio(0);\n}\n\n}  // namespace\n\n__global__")
+    s = rep(s, "      ipassA(s, lane);", "      prio3(wave_s, 0);\n      ipassA(s, lane);")
+    s = rep(s, "      ipassB(s, lane);", "      prio3(wave_s, 1);\n      ipassB(s, lane);")
+    s = rep(s, "    // layout C: r bit0", "    prio3(wave_s, 2);\n    // layout C: r bit0")
+    s = rep(s, "    // ---- phase 5: y = 4*lane", "    prio3(wave_s, 3);\n    // ---- phase 5: y = 4*lane")
+open(out, "w").write(s)

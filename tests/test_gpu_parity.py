@@ -1201,3 +1201,113 @@ def test_locator_rows_every_pattern(oracle):
             ep = oracle.error_poly(erased, n)[:n].astype(np.int64) % 65535
             assert ((el[b].astype(np.int64) % 65535) == ep).all(), (nv, b)
 
+
+
+@pytest.mark.parametrize("nv", [6, 16, 100, 1024])
+def test_systematic_tiny_boundaries(oracle, nv):
+    """the per-call decode from exactly the k systematic shards
+    (systematic_tiny when k * shard_len <= 2048 B rides in the kernel
+    arguments, else systematic_g) on each side of its size limit and of the
+    64 / 512 B marks, through ECCR_reconstruct and
+    ECCR_reconstruct_from_systematic, against the reference."""
+    n, k, thr = E.code_params(nv)
+    slens = set()
+    for mark in (64, 512, 2048):
+        s = max(2, mark // k // 2 * 2)
+        slens.update(x for x in (s - 2, s, s + 2) if x >= 2)
+    rng = np.random.default_rng(nv)
+    for sl in sorted(slens):
+        for plen in sorted({k * sl, max(1, k * (sl - 2) + 1)}):
+            assert E.shard_len(nv, plen) == sl, (nv, plen, sl)
+            p = rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+            sh = E.obtain_chunks(nv, p)
+            ref = oracle.reconstruct_from_systematic(nv, sh[:k])
+            assert ref[:plen] == p
+            assert E.reconstruct_from_systematic(nv, [(i, sh[i]) for i in range(k)]) == ref, (nv, plen)
+            assert E.reconstruct(nv, [(i, sh[i]) for i in range(k)]) == ref, (nv, plen)
+
+
+def test_encode_ws_without_counter(oracle):
+    """a workspace below the queried size (here NULL / 0 bytes, as a
+    caller that cached an older size would pass) runs the k = 256 / 512 / 1024
+    encodes on their static tile schedule instead of failing; bit-exact."""
+    import torch
+    for nv, plen, B in ((1024, 70_000, 5), (600, 50_000, 3), (2500, 60_000, 3), (4096, 80_000, 3)):
+        n, k, thr = E.code_params(nv)
+        assert E.workspace_bytes(nv, plen, B)[0] == 256, nv
+        sl = E.shard_len(nv, plen)
+        ss = (sl + 63) // 64 * 64
+        pays = [synth.payload(nv * 7 + b, plen) for b in range(B)]
+        d_pay = torch.from_numpy(np.stack(pays)).cuda()
+        d_sh = torch.zeros((B, nv, ss), dtype=torch.uint8, device="cuda")
+        E.encode_batch_ws(nv, d_pay, plen, plen, B, d_sh, ss, None)
+        torch.cuda.synchronize()
+        got = d_sh.cpu().numpy()
+        for b in range(B):
+            want = oracle.encode(nv, pays[b].tobytes())
+            assert all(got[b, i, :sl].tobytes() == want[i] for i in range(nv)), (nv, b)
+
+
+def test_stream_scratch_eviction_many_streams():
+    """more streams than the 64 kept scratch buffers.  84 streams
+    issue plain batch calls (the n = 1024 reconstruct keeps its gather order in
+    its stream's scratch), so 20 are evicted and the evicted buffers are freed
+    in one implicit drain (16 at a time); the first streams, evicted by then,
+    run again (new buffers) and every round trip holds."""
+    import ctypes
+    import torch
+    # distinct HIP streams (torch.cuda.Stream() hands out a pool of 32)
+    hip = ctypes.CDLL("libamdhip64.so")
+    raw = []
+    for _ in range(84):
+        h = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+        raw.append(h)
+    streams = [torch.cuda.ExternalStream(h.value) for h in raw]
+    for j, s in enumerate(streams):
+        with torch.cuda.stream(s):
+            pay, pres, sh, el, out = _batch_case(1024, 20_001, 2, seed0=900 + j, pad=64)
+        assert (out[:, :20_001] == pay).all(), j
+    for j, s in enumerate(streams[:8]):  # evicted: allocated again
+        with torch.cuda.stream(s):
+            pay, pres, sh, el, out = _batch_case(1024, 30_001, 2, seed0=990 + j, pad=64)
+        assert (out[:, :30_001] == pay).all(), j
+    torch.cuda.synchronize()
+    kept = sum(E.release_stream_scratch(s) for s in streams)
+    assert kept == 64, kept  # the 64 most recent streams hold one each
+    for h in raw:
+        assert hip.hipStreamDestroy(h) == 0
+
+
+def test_release_stream_scratch_while_leased():
+    """ECCR_AMD_release_stream_scratch from one thread while another
+    thread's plain calls lease that stream's scratch: a release waits for the
+    lease holder to finish enqueueing, a buffer still held goes to the dead
+    list, and every call's results stay exact."""
+    import threading
+    import time
+    import torch
+    s = torch.cuda.Stream()
+    errs, done = [], threading.Event()
+
+    def caller():
+        try:
+            for rep in range(12):
+                with torch.cuda.stream(s):
+                    pay, pres, sh, el, out = _batch_case(1024, 40_001 + 2 * rep, 2, seed0=70 + rep, pad=64)
+                assert (out[:, :40_001 + 2 * rep] == pay).all(), rep
+        except Exception as e:  # reported by the main thread
+            errs.append(e)
+        finally:
+            done.set()
+
+    t = threading.Thread(target=caller)
+    t.start()
+    releases = 0
+    while not done.is_set():
+        releases += E.release_stream_scratch(s)
+        time.sleep(0.002)
+    t.join(120)
+    assert not t.is_alive() and not errs, errs
+    torch.cuda.synchronize()
+    E.release_stream_scratch(s)

@@ -38,11 +38,16 @@ def _torchrun(script_args, timeout=300):
 
 def test_bench_two_ranks_share_gpu():
     r, line = _torchrun(["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
-                         "--batch", "48", "--payload", "100000", "--no-cpu-baseline"])
+                         "--batch", "48", "--payload", "100000", "--no-cpu-baseline",
+                         "--e2e-batch", "8", "--e2e-per-size", "2", "--e2e-reps", "1"])
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     assert line is not None and line["roundtrip_ok"], line
     assert line["config"]["parallelism"] == "dp2" and "gloo" in line["rehearsal"]
     assert line["value"] > 0 and line["steps"] == 2
+    # the host-resident block ran on both ranks (max-over-ranks time)
+    e = line["e2e"]
+    assert e["config2"]["roundtrip_ok"] and e["config5_mixed"]["roundtrip_ok"], e
+    assert e["config2"]["batch_per_gpu"] == 8 and e["config5_mixed"]["payloads"] == 12, e
 
 
 def test_bench_gpus_flag_launches_ranks():
@@ -53,7 +58,7 @@ def test_bench_gpus_flag_launches_ranks():
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
-           "--batch", "48", "--payload", "100000", "--no-cpu-baseline", "--sweep", "none"]
+           "--batch", "48", "--payload", "100000", "--no-cpu-baseline", "--sweep", "none", "--no-e2e"]
     r = subprocess.run(["timeout", "-k", "10", "300"] + cmd, cwd=ROOT, env=env,
                        capture_output=True, text=True)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
@@ -76,3 +81,28 @@ def test_bench_stream_two_ranks_share_gpu():
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     assert line is not None and line["roundtrip_ok"], line
     assert line["my_payloads"] >= 1 and "gloo" in line["rehearsal"]
+
+
+def test_bench_e2e_block_one_rank():
+    """the driver-run bench line carries the host-resident
+    (PCIe-inclusive) rates, config 2 shape and the config-5 size mix, each next
+    to the PCIe bound from this box's measured pinned copy rates."""
+    cmd = [sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--batch", "32",
+           "--payload", "1000000", "--no-cpu-baseline", "--sweep", "none",
+           "--e2e-batch", "16", "--e2e-per-size", "2", "--e2e-reps", "1"]
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run(["timeout", "-k", "10", "300"] + cmd, cwd=ROOT, env=env,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    e = line["e2e"]
+    p = e["pcie_measured"]
+    assert min(p["h2d_GBps"], p["d2h_GBps"], p["duplex_GBps"]) > 1, p
+    for leg in ("config2", "config5_mixed"):
+        assert e[leg]["roundtrip_ok"], e[leg]
+        assert e[leg]["roundtrip_GiBps"] > 0
+        # the bound is a bound: no measured rate above it (5% timing slack)
+        assert 0 < e[leg]["frac_of_pcie_bound"] <= 1.05, e[leg]
+    assert e["config2"]["batch_per_gpu"] == 16 and e["config5_mixed"]["payloads"] == 12

@@ -22,7 +22,7 @@ def test_stamp_variant_applies(kind, tmp_path):
     assert "STAMP(" in src and "ECCR_DIAG_stamps" in src
 
 
-@pytest.mark.parametrize("kind", ["nobar", "nost", "nold", "nostg", "stplain", "noprio", "notab", "cmp",
+@pytest.mark.parametrize("kind", ["nobar", "nbread", "nbstg", "static", "nobar+static", "cmp+static", "nost", "nold", "nostg", "stplain", "noprio", "notab", "cmp",
                                   "cmpt", "clk", "clk+nostg", "clk+cmp"])
 def test_enc_diag_variant_applies(kind, tmp_path):
     r = subprocess.run([sys.executable, os.path.join(VAR, "enc_diag.py"), kind, str(tmp_path)],
@@ -36,3 +36,22 @@ def test_product_sources_have_no_diag_switches():
     for f in os.listdir(csrc):
         text = open(os.path.join(csrc, f)).read()
         assert "g_stamp" not in text and "ECCR_DIAG" not in text, f
+
+
+@pytest.mark.parametrize("knobs", ["RA=3,RB=5", "RVLATE=1", "PRIO=1", "PRIO=2", "RA=4,RB=7,RVLATE=1,PRIO=2"])
+def test_n1024x_knob_variant_applies(knobs, tmp_path):
+    """reconstruct_n1024x's tuning switches live in
+    scripts/variants/n1024x_knobs.py, not in the product source."""
+    out = tmp_path / "dec_n1024x.hip"
+    r = subprocess.run([sys.executable, os.path.join(VAR, "n1024x_knobs.py"), knobs, str(out)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    src = out.read_text()
+    assert ("prio3(wave_s, 3)" in src) == ("PRIO" in knobs)
+
+
+def test_product_sources_have_no_tuning_macros():
+    csrc = os.path.join(ROOT, "erasure-coding-crust_amd", "csrc")
+    for f in os.listdir(csrc):
+        text = open(os.path.join(csrc, f)).read()
+        assert "N1024X_" not in text, f
