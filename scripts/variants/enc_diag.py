@@ -10,6 +10,9 @@ that work costs in the real interleaving:
             barriers dropped the tickets are read unsynchronised (lagging
             waves skip or repeat tiles), so combine nobar / cmp with static
             for a time account (nobar+static, cmp+static)
+    wdyn    every wave takes its own tiles (its 8-piece group of the tile) from a
+            counter of its own: no cross-wave tile hand-off, so nobar / cmp
+            stay balanced and valid for timing (nobar+wdyn, cmp+wdyn)
     nbread  only the "regions read out" barriers dropped (tile start, after
             IFFT pass A, before each coset's first exchange)
     nbstg   only the "rows staged" barriers dropped (before each store phase)
@@ -27,6 +30,9 @@ that work costs in the real interleaving:
     xnobar, xnogat, xnoout  the same three for reconstruct_n1024x (writes
             OUTDIR/dec_n1024x.hip)
     xnorv   reconstruct_n1024x: phase 5's re-read of the present rows dropped
+    xwdyn   reconstruct_n1024x: every wave takes its own tiles (its 4-column
+            group) from a counter of its own (one 128-B line each): with
+            xnobar / xnogat the waves stay balanced and the timing valid
     kclk:F  the clk probe in the kernel of csrc file F (its first kernel with
             dynamic LDS), e.g. kclk:enc_k1024.hip (writes OUTDIR/F)
     dclk    the clk probe in reconstruct_n1024 instead (writes OUTDIR/dec_n1024.hip;
@@ -89,6 +95,20 @@ for k in kinds:
     elif k == "static":
         enc = rep(enc, "  uint32_t cur = __builtin_amdgcn_readfirstlane(*slot);", "  uint32_t cur = blockIdx.x;")
         enc = rep(enc, "      next = __builtin_amdgcn_readfirstlane(*slot);", "      next = cur + gridDim.x;")
+    elif k == "wdyn":
+        take = ("[&]() { uint32_t v_ = 0; if ((tid0 & 63) == 0) v_ = atomicAdd(tick + 32 + 32 * (tid0 >> 6), 1u);"
+                " return __builtin_amdgcn_readfirstlane(v_); }()")
+        enc = rep(enc, "  uint32_t cur = __builtin_amdgcn_readfirstlane(*slot);", f"  uint32_t cur = {take};")
+        # the next tile's ticket taken at the tile start (lane 0 of each wave),
+        # read at its end: the atomic's latency hidden as in the product
+        enc = rep(enc, "    if (tid0 == 0) taken = tick ? atomicAdd(tick, 1u) : cur + gridDim.x;",
+                  "    if ((tid0 & 63) == 0) taken = atomicAdd(tick + 32 + 32 * (tid0 >> 6), 1u);")
+        enc = rep(enc, "      next = __builtin_amdgcn_readfirstlane(*slot);", "      next = __builtin_amdgcn_readfirstlane(taken);")
+        # one counter per wave index, each on its own 128-B line (8 on one
+        # line serialise in L2: ~6 ns per atomic); 1152 B of scratch
+        enc = rep(enc, "launch_zero_counters(tick, sizeof(uint32_t), s)", "launch_zero_counters(tick, 1152, s)")
+        extra["enc_k256.hip"] = rep(open(f"{CS}/enc_k256.hip").read(),
+                                    "return p.n == 1024 ? 256 : 0;", "return p.n == 1024 ? 1152 : 0;")
     elif k == "nbread":
         for old in ("    rsync();  // the other waves are done reading this region (last tile)\n",
                     "    rsync();  // systematic rows read out of the regions\n",
@@ -132,7 +152,7 @@ for k in kinds:
                   "        asm volatile(\"\" :: \"v\"(w0), \"v\"(w1), \"v\"(O + (col * K + 4 * lane) * 2));\n")
     elif k == "xnobar":
         decx = rep(decx, "      lds_barrier();  // the previous tile's readers of the regions are done\n", "")
-        decx = rep(decx, "    __syncthreads();\n    const uint64_t cbase", "    const uint64_t cbase")
+        decx = rep(decx, "    __syncthreads();  // (every wave has read SLOT)\n    const uint64_t cbase", "    const uint64_t cbase")
         extra["dec_n1024x.hip"] = decx
     elif k == "xnogat":
         decx = rep(decx, "      if ((meta[0] & 0xffffu) != 0xffffu) load_row(0);\n", "")
@@ -142,6 +162,19 @@ for k in kinds:
     elif k == "xnorv":
         decx = rep(decx, "          rv[q] = whole ? *reinterpret_cast<const uint2 *>(row) : load8_any(row, uint32_t(2 * (ncols - cbase)));\n",
                    "          rv[q] = make_uint2(uint32_t(reinterpret_cast<uintptr_t>(row)), q);\n")
+        extra["dec_n1024x.hip"] = decx
+    elif k == "xwdyn":
+        W = "(tid0 & 63) == 0"
+        decx = rep(decx, "  if (tid0 == 0) taken = gridDim.x + atomicAdd(tick, 1u);\n",
+                   f"  if ({W}) taken = gridDim.x + atomicAdd(tick + 32 + 32 * (tid0 >> 6), 1u);\n")
+        decx = rep(decx, "  if (tid0 == 0) *slot = taken;  // read after the first tile's region barrier\n", "")
+        decx = rep(decx, "      nxt = __builtin_amdgcn_readfirstlane(*slot);\n"
+                         "      if (tid0 == 0) taken = gridDim.x + atomicAdd(tick, 1u);  // the tile after nxt\n",
+                   "      nxt = __builtin_amdgcn_readfirstlane(taken);\n"
+                   f"      if ({W}) taken = gridDim.x + atomicAdd(tick + 32 + 32 * (tid0 >> 6), 1u);\n")
+        decx = rep(decx, "    if (tid0 == 0) *slot = taken;\n", "")
+        decx = rep(decx, "return n1024_tick_offset(p, batch) + 256; }", "return n1024_tick_offset(p, batch) + 2048; }")
+        decx = rep(decx, "launch_zero_counters(tick, sizeof(uint32_t), s)", "launch_zero_counters(tick, 2048, s)")
         extra["dec_n1024x.hip"] = decx
     elif k == "xnoout":
         decx = rep(decx, "        *reinterpret_cast<uint2 *>(O + (col * K + 4 * lane) * 2) = make_uint2(w0, w1);\n",

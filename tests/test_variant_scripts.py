@@ -22,7 +22,7 @@ def test_stamp_variant_applies(kind, tmp_path):
     assert "STAMP(" in src and "ECCR_DIAG_stamps" in src
 
 
-@pytest.mark.parametrize("kind", ["nobar", "nbread", "nbstg", "static", "nobar+static", "cmp+static", "nost", "nold", "nostg", "stplain", "noprio", "notab", "cmp",
+@pytest.mark.parametrize("kind", ["nobar", "nbread", "nbstg", "static", "nobar+static", "cmp+static", "cmp+wdyn", "nobar+wdyn", "xnobar+xnogat+xnoout+xwdyn", "xnobar+xwdyn", "xnobar", "xnogat", "xnorv", "xnoout", "nost", "nold", "nostg", "stplain", "noprio", "notab", "cmp",
                                   "cmpt", "clk", "clk+nostg", "clk+cmp"])
 def test_enc_diag_variant_applies(kind, tmp_path):
     r = subprocess.run([sys.executable, os.path.join(VAR, "enc_diag.py"), kind, str(tmp_path)],
