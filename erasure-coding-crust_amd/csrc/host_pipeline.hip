@@ -52,19 +52,23 @@ __global__ void __launch_bounds__(256) scatter_present(const uint8_t *__restrict
 
 struct Slot {
   hipStream_t stream = nullptr;
-  uint8_t *d_a = nullptr, *d_b = nullptr, *d_c = nullptr, *d_present = nullptr;
+  uint8_t *d_a = nullptr, *d_b = nullptr, *d_c = nullptr;
   uint16_t *d_elog = nullptr, *d_idx = nullptr;
-  uint32_t *d_pat = nullptr;
+  // a chunk's pattern index ([cb] u32) then its distinct present rows
+  // ([npat][n]) in one device buffer, uploaded by ONE copy from the pinned
+  // h_meta (round 6: two copies from pageable vectors, staged by the runtime,
+  // cost ~15% of the config-2 reconstruct's PCIe-bound time)
+  uint8_t *d_meta = nullptr, *h_meta = nullptr;
+  size_t cap_meta = 0, cap_h_meta = 0;
   // the slot's own kernel scratch (k = 1024 encode coefficients, reconstruct
   // gather orders): stream-ordered by the slot, so the three slots overlap; a
   // shared per-device lease would order them behind each other
   uint8_t *d_scr = nullptr;
-  size_t cap_a = 0, cap_b = 0, cap_c = 0, cap_present = 0, cap_elog = 0, cap_idx = 0, cap_pat = 0,
-         cap_scr = 0;
-  // host staging of a chunk's distinct erasure patterns; `staged` is recorded
-  // after their upload so the next chunk on this slot does not overwrite them early
+  size_t cap_a = 0, cap_b = 0, cap_c = 0, cap_elog = 0, cap_idx = 0, cap_scr = 0;
+  // host staging of a chunk's distinct erasure patterns (h_rows, then copied
+  // into h_meta); `staged` is recorded after h_meta's upload so the next chunk
+  // on this slot does not overwrite it early
   std::vector<uint8_t> h_rows;
-  std::vector<uint32_t> h_pat;
   hipEvent_t staged = nullptr;
 };
 
@@ -85,10 +89,10 @@ struct Pipeline {
       }
       if (s.staged) (void)hipEventDestroy(s.staged);
       for (void *p : {static_cast<void *>(s.d_a), static_cast<void *>(s.d_b), static_cast<void *>(s.d_c),
-                      static_cast<void *>(s.d_present), static_cast<void *>(s.d_elog),
-                      static_cast<void *>(s.d_idx), static_cast<void *>(s.d_pat),
-                      static_cast<void *>(s.d_scr)})
+                      static_cast<void *>(s.d_meta), static_cast<void *>(s.d_elog),
+                      static_cast<void *>(s.d_idx), static_cast<void *>(s.d_scr)})
         if (p) (void)hipFree(p);
+      if (s.h_meta) (void)hipHostFree(s.h_meta);
       s = Slot{};
     }
     if (switched) (void)hipSetDevice(cur);
@@ -282,15 +286,19 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
   for (unsigned long c0 = 0, i = 0; c0 < batch; c0 += chunk, ++i) {
     Slot &s = pl->slot[i % kSlots];
     const size_t cb = batch - c0 < chunk ? batch - c0 : chunk;
+    const size_t pat_bytes = (chunk * 4 + 255) / 256 * 256;  // the present rows start 256-B aligned
     if (!grow(&s.d_a, &s.cap_a, chunk * cnt * sstride) || !grow(&s.d_b, &s.cap_b, chunk * nv * dss) ||
-        !grow(&s.d_c, &s.cap_c, chunk * dos) || !grow(&s.d_present, &s.cap_present, chunk * p.n) ||
-        !grow(&s.d_elog, &s.cap_elog, chunk * p.n * 2) ||
-        !grow(&s.d_idx, &s.cap_idx, chunk * cnt * 2) || !grow(&s.d_pat, &s.cap_pat, chunk * 4))
+        !grow(&s.d_c, &s.cap_c, chunk * dos) || !grow(&s.d_meta, &s.cap_meta, pat_bytes + chunk * p.n) ||
+        !grow(&s.d_elog, &s.cap_elog, chunk * p.n * 2) || !grow(&s.d_idx, &s.cap_idx, chunk * cnt * 2))
       return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+    uint32_t *d_pat = reinterpret_cast<uint32_t *>(s.d_meta);
+    uint8_t *d_present = s.d_meta + pat_bytes;
     // distinct erasure patterns of the chunk: one present
     // row and one locator each; payload b uses row h_pat[b]
     if (!ok(hipEventSynchronize(s.staged), "staging reuse")) return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-    s.h_pat.resize(cb);
+    if (!ensure_host(&s.h_meta, &s.cap_h_meta, pat_bytes + chunk * p.n))
+      return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+    uint32_t *h_pat = reinterpret_cast<uint32_t *>(s.h_meta);
     s.h_rows.clear();
     s.h_rows.reserve(cb * p.n);
     // hash -> first pattern with it; further ones chained through next_pat
@@ -303,7 +311,7 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
       const size_t b = c0 + j;
       const uint16_t *ix = h_index + b * cnt;
       if (j > 0 && std::memcmp(ix, ix - cnt, cnt * 2) == 0) {  // same list as the previous payload
-        s.h_pat[j] = s.h_pat[j - 1];
+        h_pat[j] = h_pat[j - 1];
         continue;
       }
       int32_t found = -1;
@@ -327,8 +335,9 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
         uint8_t *row = s.h_rows.data() + size_t(found) * p.n;
         for (unsigned long t = 0; t < cnt; ++t) row[ix[t]] = 1;
       }
-      s.h_pat[j] = uint32_t(found);
+      h_pat[j] = uint32_t(found);
     }
+    std::memcpy(s.h_meta + pat_bytes, s.h_rows.data(), size_t(npat) * p.n);
     void *scratch = nullptr;
     if (!slot_scratch(s, reconstruct_scratch_bytes(p, slen, cb), &scratch))
       return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
@@ -339,11 +348,9 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
         ok(hipMemcpyAsync(s.d_idx, h_index + c0 * cnt, cb * cnt * 2, hipMemcpyHostToDevice,
                           s.stream),
            "H2D index") &&
-        ok(hipMemcpyAsync(s.d_present, s.h_rows.data(), size_t(npat) * p.n, hipMemcpyHostToDevice,
+        ok(hipMemcpyAsync(s.d_meta, s.h_meta, pat_bytes + size_t(npat) * p.n, hipMemcpyHostToDevice,
                           s.stream),
            "H2D patterns") &&
-        ok(hipMemcpyAsync(s.d_pat, s.h_pat.data(), cb * 4, hipMemcpyHostToDevice, s.stream),
-           "H2D pattern index") &&
         ok(hipEventRecord(s.staged, s.stream), "staging event");
     if (good) {
       hipLaunchKernelGGL(scatter_present, dim3(unsigned(cnt), unsigned(cb < 65535 ? cb : 65535)), dim3(256),
@@ -351,10 +358,10 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
                          s.d_b, uint64_t(dss), uint32_t(nv), static_cast<uint8_t *>(nullptr),
                          uint32_t(p.n), uint32_t(cb));
       good = ok(hipGetLastError(), "scatter launch") &&
-             ok(launch_error_locator(p, s.d_present, npat, fold, nullptr, s.d_elog, s.stream),
+             ok(launch_error_locator(p, d_present, npat, fold, nullptr, s.d_elog, s.stream),
                 "error locator launch") &&
-             ok(launch_reconstruct(p, device_tables(d), s.d_b, slen, dss, s.d_present, s.d_elog,
-                                   s.d_pat, cb, s.d_c, dos, scratch, s.stream),
+             ok(launch_reconstruct(p, device_tables(d), s.d_b, slen, dss, d_present, s.d_elog,
+                                   d_pat, cb, s.d_c, dos, scratch, s.stream),
                 "reconstruct launch") &&
              ok(out_lin ? hipMemcpyAsync(h_out + c0 * ostride, s.d_c, (cb - 1) * ostride + ob,
                                          hipMemcpyDeviceToHost, s.stream)
