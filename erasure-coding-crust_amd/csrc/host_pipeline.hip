@@ -53,18 +53,18 @@ __global__ void __launch_bounds__(256) scatter_present(const uint8_t *__restrict
 struct Slot {
   hipStream_t stream = nullptr;
   uint8_t *d_a = nullptr, *d_b = nullptr, *d_c = nullptr;
-  uint16_t *d_elog = nullptr, *d_idx = nullptr;
-  // a chunk's pattern index ([cb] u32) then its distinct present rows
-  // ([npat][n]) in one device buffer, uploaded by ONE copy from the pinned
-  // h_meta (round 6: two copies from pageable vectors, staged by the runtime,
-  // cost ~15% of the config-2 reconstruct's PCIe-bound time)
+  uint16_t *d_elog = nullptr;
+  // a chunk's pattern index ([cb] u32), its shards' indices ([cb][cnt]
+  // u16) and its distinct present rows ([npat][n]) in one device buffer,
+  // uploaded by ONE copy from the pinned h_meta (until round 6: three copies,
+  // two of them from pageable vectors, beside the shards' copy)
   uint8_t *d_meta = nullptr, *h_meta = nullptr;
   size_t cap_meta = 0, cap_h_meta = 0;
   // the slot's own kernel scratch (k = 1024 encode coefficients, reconstruct
   // gather orders): stream-ordered by the slot, so the three slots overlap; a
   // shared per-device lease would order them behind each other
   uint8_t *d_scr = nullptr;
-  size_t cap_a = 0, cap_b = 0, cap_c = 0, cap_elog = 0, cap_idx = 0, cap_scr = 0;
+  size_t cap_a = 0, cap_b = 0, cap_c = 0, cap_elog = 0, cap_scr = 0;
   // host staging of a chunk's distinct erasure patterns (h_rows, then copied
   // into h_meta); `staged` is recorded after h_meta's upload so the next chunk
   // on this slot does not overwrite it early
@@ -90,7 +90,7 @@ struct Pipeline {
       if (s.staged) (void)hipEventDestroy(s.staged);
       for (void *p : {static_cast<void *>(s.d_a), static_cast<void *>(s.d_b), static_cast<void *>(s.d_c),
                       static_cast<void *>(s.d_meta), static_cast<void *>(s.d_elog),
-                      static_cast<void *>(s.d_idx), static_cast<void *>(s.d_scr)})
+                      static_cast<void *>(s.d_scr)})
         if (p) (void)hipFree(p);
       if (s.h_meta) (void)hipHostFree(s.h_meta);
       s = Slot{};
@@ -100,11 +100,11 @@ struct Pipeline {
   }
 };
 
-// chunk = 0: payloads per pipeline step such that a step moves ~16 MB over
+// chunk = 0: payloads per pipeline step such that a step moves ~32 MB over
 // the link (small payloads: few large copies instead of many latency-bound
 // ones; large payloads: still >= 3 steps in flight when the batch allows)
 unsigned long auto_chunk(size_t bytes_per_payload, unsigned long batch) {
-  const size_t target = size_t(16) << 20;
+  const size_t target = size_t(32) << 20;
   size_t c = bytes_per_payload ? target / bytes_per_payload : batch;
   if (c < 1) c = 1;
   if (batch >= 3 && c > (batch + 2) / 3 && bytes_per_payload * ((batch + 2) / 3) >= (size_t(4) << 20))
@@ -286,18 +286,22 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
   for (unsigned long c0 = 0, i = 0; c0 < batch; c0 += chunk, ++i) {
     Slot &s = pl->slot[i % kSlots];
     const size_t cb = batch - c0 < chunk ? batch - c0 : chunk;
-    const size_t pat_bytes = (chunk * 4 + 255) / 256 * 256;  // the present rows start 256-B aligned
+    // h_meta / d_meta: [pattern index | shard indices | present rows], each part 256-B aligned
+    const size_t pat_bytes = (chunk * 4 + 255) / 256 * 256, idx_bytes = (chunk * cnt * 2 + 255) / 256 * 256;
+    const size_t rows_at = pat_bytes + idx_bytes;
     if (!grow(&s.d_a, &s.cap_a, chunk * cnt * sstride) || !grow(&s.d_b, &s.cap_b, chunk * nv * dss) ||
-        !grow(&s.d_c, &s.cap_c, chunk * dos) || !grow(&s.d_meta, &s.cap_meta, pat_bytes + chunk * p.n) ||
-        !grow(&s.d_elog, &s.cap_elog, chunk * p.n * 2) || !grow(&s.d_idx, &s.cap_idx, chunk * cnt * 2))
+        !grow(&s.d_c, &s.cap_c, chunk * dos) || !grow(&s.d_meta, &s.cap_meta, rows_at + chunk * p.n) ||
+        !grow(&s.d_elog, &s.cap_elog, chunk * p.n * 2))
       return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
     uint32_t *d_pat = reinterpret_cast<uint32_t *>(s.d_meta);
-    uint8_t *d_present = s.d_meta + pat_bytes;
+    const uint16_t *d_idx = reinterpret_cast<const uint16_t *>(s.d_meta + pat_bytes);
+    uint8_t *d_present = s.d_meta + rows_at;
     // distinct erasure patterns of the chunk: one present
     // row and one locator each; payload b uses row h_pat[b]
     if (!ok(hipEventSynchronize(s.staged), "staging reuse")) return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
-    if (!ensure_host(&s.h_meta, &s.cap_h_meta, pat_bytes + chunk * p.n))
+    if (!ensure_host(&s.h_meta, &s.cap_h_meta, rows_at + chunk * p.n))
       return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
+    std::memcpy(s.h_meta + pat_bytes, h_index + c0 * cnt, cb * cnt * 2);
     uint32_t *h_pat = reinterpret_cast<uint32_t *>(s.h_meta);
     s.h_rows.clear();
     s.h_rows.reserve(cb * p.n);
@@ -337,7 +341,7 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
       }
       h_pat[j] = uint32_t(found);
     }
-    std::memcpy(s.h_meta + pat_bytes, s.h_rows.data(), size_t(npat) * p.n);
+    std::memcpy(s.h_meta + rows_at, s.h_rows.data(), size_t(npat) * p.n);
     void *scratch = nullptr;
     if (!slot_scratch(s, reconstruct_scratch_bytes(p, slen, cb), &scratch))
       return res(NPRS_RESULT_UNKNOWN_RECONSTRUCTION);
@@ -345,16 +349,13 @@ NPRSResult ECCR_AMD_reconstruct_host_batch(unsigned long nv, const uint8_t *h_sh
         ok(hipMemcpyAsync(s.d_a, h_shards + c0 * cnt * sstride, cb * cnt * sstride,
                           hipMemcpyHostToDevice, s.stream),
            "H2D shards") &&
-        ok(hipMemcpyAsync(s.d_idx, h_index + c0 * cnt, cb * cnt * 2, hipMemcpyHostToDevice,
-                          s.stream),
-           "H2D index") &&
-        ok(hipMemcpyAsync(s.d_meta, s.h_meta, pat_bytes + size_t(npat) * p.n, hipMemcpyHostToDevice,
+        ok(hipMemcpyAsync(s.d_meta, s.h_meta, rows_at + size_t(npat) * p.n, hipMemcpyHostToDevice,
                           s.stream),
            "H2D patterns") &&
         ok(hipEventRecord(s.staged, s.stream), "staging event");
     if (good) {
       hipLaunchKernelGGL(scatter_present, dim3(unsigned(cnt), unsigned(cb < 65535 ? cb : 65535)), dim3(256),
-                         0, s.stream, s.d_a, uint64_t(sstride), s.d_idx, uint32_t(cnt), uint64_t(slen),
+                         0, s.stream, s.d_a, uint64_t(sstride), d_idx, uint32_t(cnt), uint64_t(slen),
                          s.d_b, uint64_t(dss), uint32_t(nv), static_cast<uint8_t *>(nullptr),
                          uint32_t(p.n), uint32_t(cb));
       good = ok(hipGetLastError(), "scatter launch") &&
