@@ -403,9 +403,7 @@ reconstruct_n4096(
         const uint32_t W = 2 * MPW * wave + j, l = lane ^ (W & 15);
         const uint32_t yy = l >> 2;
         if ((pw[j >> 1] >> (16 * (j & 1) + yy)) & 1)
-          __builtin_amdgcn_global_load_lds(
-              (const __attribute__((address_space(1))) void *)(SH + uint64_t(16 * W + yy) * sstride + 2 * col0 + 16 * (l & 3)),
-              (__attribute__((address_space(3))) void *)(regions + 1024 * W), 16, 0, 0);
+          lds_dma16(lds_addr(regions) + 1024 * W, SH + uint64_t(16 * W + yy) * sstride + 2 * col0 + 16 * (l & 3));
       }
     }
     // k < 1024: mask dwords (lane >> 4) + 4 m (rows y0 = 2 lane + 128 m + (0, 1))

@@ -65,6 +65,24 @@ __device__ __forceinline__ void lds_st2(uint32_t a, uint2 v) {
   *(__attribute__((address_space(3))) uint64_t *)(uintptr_t(a)) = (uint64_t(v.y) << 32) | v.x;
 }
 
+// One LDS-DMA wave-instruction: 16 B per lane from `src` (per lane) to the
+// wave's 1 KB of LDS at `dst` (wave-uniform: M0) + 16 lane.  Inline asm
+// instead of __builtin_amdgcn_global_load_lds: the compiler treats a pending
+// LDS-DMA as a write to every LDS address and waits for it with vmcnt(0)
+// before the next LDS access it cannot prove disjoint, which also waits for
+// every shard store issued after the DMA (enc_k1024: before each coset's first
+// table read, right after the previous coset's row stores).  Hidden from the
+// compiler, the DMA is retired only by the kernels' own s_waitcnt vmcnt(N)
+// before the barrier that precedes the first read of its bytes; the
+// compiler's own vmcnt waits stay correct (the counter retires in issue
+// order, so an op it does not know of only makes its waits stricter).
+__device__ __forceinline__ void lds_dma16(uint32_t dst, const void *src) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane(dst)), "v"(src)
+               : "memory");  // (M0 is reserved: the compiler sets it before each of its own uses)
+}
+
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -357,10 +375,12 @@ struct LdsTabs {
       reinterpret_cast<uint4 *>(base)[tid + k * THREADS] = make_uint4(v[k][0], v[k][1], v[k][2], v[k][3]);
   }
   // the same copy by LDS-DMA (global_load_lds_dwordx4): no VGPRs, completes in
-  // the background; the caller retires it (s_waitcnt vmcnt(0)) before the
+  // the background; the caller retires it (s_waitcnt vmcnt) before the
   // barrier that precedes the first table read.  A wave-instruction writes 1 KB
-  // of LDS linearly, which is exactly the image layout.
-  template <int THREADS>
+  // of LDS linearly, which is exactly the image layout.  Issued by lds_dma16
+  // (inline asm), so the compiler's wait model does not see it: see there.
+  // HIDDEN = false: the compiler's builtin (and its conservative waits)
+  template <int THREADS, bool HIDDEN = true>
   __device__ static __forceinline__ void dma_image(uint8_t *base, const uint8_t *img,
                                                    uint32_t tid) {
     constexpr int kChunks = kBytes / 16;
@@ -372,8 +392,11 @@ struct LdsTabs {
 #pragma unroll
     for (int k = 0; k < kChunks / THREADS; ++k) {
       const uint32_t off = (uint32_t(k) * THREADS + wave * 64) * 16;  // this wave's 1 KB slice
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(img + off + loff),
-                                       (__attribute__((address_space(3))) void *)(base + off), 16, 0, 0);
+      if constexpr (HIDDEN)
+        lds_dma16(lds_addr(base) + off, img + off + loff);
+      else
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(img + off + loff),
+                                         (__attribute__((address_space(3))) void *)(base + off), 16, 0, 0);
     }
   }
   // cooperative gather of ENTRIES tables, entry i <- mtab[src(i)], all index

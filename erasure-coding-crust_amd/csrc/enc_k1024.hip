@@ -217,7 +217,10 @@ __global__ void __launch_bounds__(THREADS)
     if (tid0 == 0) *slot = taken;  // (issued at the tile start: long returned)
     lds_barrier();  // every wave is done with the index-0 tables
     const uint32_t next = __builtin_amdgcn_readfirstlane(*slot);
-    Tabs::dma_image<THREADS>(tabs, t.timg_t + kTabImageBytes, tid);
+    // the compiler's own LDS-DMA here (HIDDEN = false, ec_device.hpp
+    // lds_dma16): with it hidden this kernel read 3% slower in an in-process
+    // A/B (profiles/r06/NOTES.md), the other DMA users 1-3% faster
+    Tabs::dma_image<THREADS, false>(tabs, t.timg_t + kTabImageBytes, tid);
     // cs: std::integral_constant coset number (its image's subfield stages)
     const auto coset = [&](auto cs) __attribute__((always_inline)) {
       constexpr uint32_t s = decltype(cs)::value;
@@ -242,7 +245,7 @@ __global__ void __launch_bounds__(THREADS)
         stage_rows(g, my, lane);
       }
       lds_barrier();  // every wave is past its FFT and staged: the next set (index 0 after the last coset)
-      Tabs::dma_image<THREADS>(tabs, t.timg_t + (s + 1 < ncos ? s + 1 : 0) * kTabImageBytes, tid);
+      Tabs::dma_image<THREADS, false>(tabs, t.timg_t + (s + 1 < ncos ? s + 1 : 0) * kTabImageBytes, tid);
       store_rows(regions, SH, sstride, s * K, nv, piece0, npieces, wave, lane);
     };
     coset(std::integral_constant<uint32_t, 1>());
