@@ -54,6 +54,15 @@ __host__ __device__ constexpr uint32_t cimg_lin(uint32_t x) {
   return ((x >> 4) << 8) | (((x ^ (x >> 4) ^ (x >> 8)) & 15) << 4);
 }
 
+// Per-coset extension images of the k = 512 encode (enc_k512w.hip; n = 2048 /
+// 4096): the general tables its FFT_512 at coset j (index 512 j, j = 1..7)
+// needs beyond the compact image's subfield and F9 entries, element-indexed
+// like it: stage m (0, 1, 2) entry e = x - (512 j >> (m + 1)), e < 256 >> m,
+// plane q at kEImg512Stage[m] + q * (4096 >> m) + cimg_lin(e).  Coset 1 uses
+// stage 0's part (20 KB), cosets 2-3 stages 0-1 (30 KB), cosets 4-7 all.
+constexpr uint32_t kEImg512Bytes = 35840, kEImg512Cosets = 7;
+constexpr uint32_t kEImg512Stage[3] = {0, 20480, 30720};
+
 // Reduced F9 image 0 (reconstruct_n1024x, 12 waves per CU): planes 0 and 1 of
 // every slot as in the F9 image (kind 0) at 0 / 16384 (the subfield tables of
 // stages >= 2 use only those), planes 2, 3 of the stage-0 (general) and
@@ -73,6 +82,7 @@ struct DevTables {
   const uint8_t *cimg = nullptr;       // kCImgBytes, the element-indexed compact image
   const MulTab *mslot = nullptr;       // 65535, mslot[i] = mtab[skews[i]]: by skew slot, one load
   const uint8_t *dimg = nullptr;       // kDImgBytes, the reduced F9 image 0
+  const uint8_t *eimg512 = nullptr;    // kEImg512Cosets x kEImg512Bytes, the k = 512 encode's coset images
 };
 
 // Completion signal of a per-call C-ABI call fused into its last kernel: when
@@ -179,6 +189,15 @@ hipError_t launch_encode_k256w(const CodeParams &p, const DevTables &t, const ui
 bool k1024_applicable(const CodeParams &p);
 size_t k1024_scratch_bytes(size_t plen, size_t batch);
 hipError_t launch_encode_k1024(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
+                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
+                               size_t sstride, void *scratch, hipStream_t s);
+
+// k = 512, n = 2048 / 4096 (enc_k512w.hip): two 8-wave workgroups per CU on
+// the compact image and the per-coset extension images; scratch (nullable:
+// static tile schedule) the tile counter, k512w_scratch_bytes
+bool k512w_applicable(const CodeParams &p);
+size_t k512w_scratch_bytes(const CodeParams &p);
+hipError_t launch_encode_k512w(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                                size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                                size_t sstride, void *scratch, hipStream_t s);
 

@@ -24,6 +24,7 @@ struct DeviceState {
   uint8_t *timg_f9 = nullptr;
   uint8_t *cimg = nullptr;
   uint8_t *dimg = nullptr;
+  uint8_t *eimg512 = nullptr;
   MulTab *mslot = nullptr;  // mtab by skew slot (DevTables::mslot)
   std::mutex mu;
   std::map<uint32_t, uint16_t *> fold;
@@ -156,6 +157,22 @@ DeviceState *device_state() {
       !hip_ok(hipMemcpy(st->cimg, cimg.data(), cimg.size(), hipMemcpyHostToDevice),
               "upload compact image"))
     return nullptr;
+  // the k = 512 encode's per-coset extension images (ec_kernels.hpp kEImg512*):
+  // general tower tables of the elements x = (512 j >> (m + 1)) + e
+  std::vector<uint8_t> eimg(kEImg512Cosets * kEImg512Bytes, 0);
+  for (uint32_t j = 1; j <= kEImg512Cosets; ++j)
+    for (uint32_t m = 0; m < 3; ++m)
+      for (uint32_t e = 0; e < (256u >> m); ++e) {
+        const uint32_t x = ((512 * j) >> (m + 1)) + e;
+        const MulTab g = f.tower_tab(f.log[2 * x]);
+        for (uint32_t q = 0; q < 5; ++q)
+          std::memcpy(&eimg[(j - 1) * kEImg512Bytes + kEImg512Stage[m] + q * (4096 >> m) + cimg_lin(e)],
+                      &g.w[4 * q], 16);
+      }
+  if (!hip_ok(hipMalloc(&st->eimg512, eimg.size()), "hipMalloc(k512 coset images)") ||
+      !hip_ok(hipMemcpy(st->eimg512, eimg.data(), eimg.size(), hipMemcpyHostToDevice),
+              "upload k512 coset images"))
+    return nullptr;
   // the reduced F9 image 0 (ec_kernels.hpp kDImgBytes) from F9 image kind 0
   std::vector<uint8_t> dimg(kDImgBytes, 0);
   std::memcpy(dimg.data(), img_f9.data(), 2 * 16384);
@@ -220,6 +237,7 @@ DevTables device_tables(DeviceState *d) {
   t.cimg = d->cimg;
   t.mslot = d->mslot;
   t.dimg = d->dimg;
+  t.eimg512 = d->eimg512;
   return t;
 }
 

@@ -85,3 +85,18 @@ def test_dec_n1024x_no_spills(tmp_path):
     assert "scratch_" not in body
     assert re.search(r"NumVgprs:\s+(\d+)", text), "resource summary missing"
     assert all(int(v) <= 168 for v in re.findall(r"NumVgprs:\s+(\d+)", text))
+
+
+def test_enc_k512w_fast_store_count_no_spills(tmp_path):
+    # enc_k512w.hip: store_own's fast path, 4 stores per lane (the vmcnt(4)
+    # before cosets 2.. counts the previous coset's stores past the extension
+    # image's LDS-DMA); the coset loop keeps the next tile's payload out of
+    # the loop-carried state, so no scratch spills
+    src = open(os.path.join(CSRC, "enc_k512w.hip")).read()
+    assert src.count("vmcnt(4)") >= 1
+    text = _asm("enc_k512w.hip", tmp_path)
+    blocks = _nt_store_blocks(text, "encode_k512w")
+    assert blocks and all(c == 4 for c in blocks), blocks
+    body = text[text.index("encode_k512w"):]
+    body = body[:body.index("s_endpgm")]
+    assert "scratch_" not in body

@@ -205,6 +205,33 @@ def test_batch_vs_oracle(oracle, nv, plen, batch, pad):
         assert out[b].tobytes() == oracle.reconstruct(nv, keep)
 
 
+@pytest.mark.parametrize("nv,plen,batch,pad", [
+    (1534, 70001, 3, 64), (1535, 1, 2, 16), (1536, 3 * 32768, 2, 16), (1800, 33793, 2, 8),
+    (2048, 66559, 3, 64), (2049, 40001, 2, 16), (2560, 50001, 2, 64), (2561, 30001, 2, 8),
+    (3000, 32769, 2, 64), (3069, 100001, 3, 16), (3069, 1024 * 31, 2, 64)])
+def test_encode_k512w_vs_oracle(oracle, nv, plen, batch, pad):
+    """enc_k512w.hip (k = 512, n = 2048 / 4096): the first and last
+    n_validators of each coset count (J = 2..5 cosets, the last partly below
+    n_validators), payloads of one piece, of whole and partial 32-piece tiles
+    (waves with no pieces), 8 / 16 / 64-byte row pitches (the slow store path
+    below 16), against the reference encoder."""
+    import torch
+    n, k, _ = E.code_params(nv)
+    assert k == 512
+    sl = E.shard_len(nv, plen)
+    ss = (sl + pad - 1) // pad * pad
+    pays = [synth.payload(nv * 3 + b, plen) for b in range(batch)]
+    d_pay = torch.from_numpy(np.stack(pays)).cuda()
+    d_sh = torch.full((batch, nv, ss), 0x5C, dtype=torch.uint8, device="cuda")
+    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+    torch.cuda.synchronize()
+    got = d_sh.cpu().numpy()
+    for b in range(batch):
+        want = oracle.encode(nv, pays[b].tobytes())
+        assert b"".join(want) == got[b, :, :sl].tobytes(), (nv, plen, b)
+        assert (got[b, :, sl:] == 0x5C).all()  # nothing past the shard length
+
+
 def test_batch_config2_roundtrip():
     """BASELINE config 2 shape (n_validators=1024, 1 MB payloads, 342 random shards):
     size-independent round trip + batch-vs-single equality on a batch of 8."""
