@@ -1,0 +1,443 @@
+// enc_k128w.hip — encode for k = 128, n = 512 / 1024 (n_validators 382..765,
+// the Polkadot validator counts of today), two 8-wave workgroups per CU.
+//
+// encode_k256w's model (enc_k256w.hip) at k = 128: per piece
+// (256 payload bytes = 128 symbols) IFFT_128 at index 0, then FFT_128 at each
+// coset 128 j below n_validators (encodeLow, poly_encoder.hpp:217-240), radix-8
+// register passes in tower coordinates, wave-private LDS exchanges.  A wave
+// holds four byte-planar groups of 4 pieces (16 pieces), each group's 128
+// positions over 16 lanes x 8 registers.  The instance bits are i1 = lane bit 4
+// and i0 = lane bit 5; read as position bit 7 and encode_k256w's instance bit,
+// the layouts A / B / C and their exchanges are encode_k256w's, so:
+//  * layout A: registers p0..p2, layout B: p3..p5, layout C: p6 (register bit
+//    0), i1 (bit 1), p5 (bit 2) -- stage 6 runs in C on register pairs, its
+//    element x = (pos + off) >> 7 uniform;
+//  * every element is x < 512 (stage 0 at the last coset 896: < 512), so the
+//    32 KB compact image holds all tables: LDS 64 KB per workgroup;
+//  * the tile is 128 pieces (8 waves x 16), each shard row a 256-B segment,
+//    stored as 16 B per lane (two groups of one wave).
+#include <hip/hip_runtime.h>
+
+#include "ec_device.hpp"
+#include "ec_kernels.hpp"
+#include "cimg.hpp"
+#include "enc_k256_common.hpp"
+
+namespace ecamd {
+namespace {
+
+constexpr int K = 128;
+constexpr int WAVES = 8;
+constexpr int THREADS = 64 * WAVES;
+constexpr int WP = 16;                       // pieces per wave
+constexpr int TILE = WP * WAVES;             // pieces per tile
+constexpr uint32_t XCH0 = kCImgBytes;        // the wave regions follow the tables
+constexpr uint32_t XCH_BYTES = 4096;
+constexpr uint32_t SLOT = XCH0 + WAVES * XCH_BYTES;  // the next tile's index
+constexpr int LDS_BYTES = int(SLOT + 16);
+static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
+static_assert(XCH0 % (2 * XCH_BYTES) == 0, "XOR-addressed regions");
+static_assert(kCImgBytes % (16 * THREADS) == 0, "whole image chunks per thread");
+
+struct XLanes {
+  uint32_t l0, l1, l2;
+};
+template <int B0>
+__device__ __forceinline__ XLanes xlanes(uint32_t base) {
+  return {cimg_lin(base >> (B0 + 1)), cimg_lin(base >> (B0 + 2)), cimg_lin(base >> (B0 + 3))};
+}
+
+// inverse radix-8 pass at index 0: every element < 64 (subfield)
+template <int B0>
+__device__ __forceinline__ void ipass(State &s, uint32_t base) {
+  const XLanes x = xlanes<B0>(base);
+  SubTab Ta0, Tb0, Ta1, Tb1, Ta2;
+  ctab(x.l0, cimg_lin(0), Ta0);
+  ctab(x.l0, cimg_lin(1), Tb0);
+  ibfly(s, 0, 1, Ta0);
+  ctab(x.l0, cimg_lin(2), Ta0);
+  ibfly(s, 2, 3, Tb0);
+  ctab(x.l0, cimg_lin(3), Tb0);
+  ibfly(s, 4, 5, Ta0);
+  ctab(x.l1, cimg_lin(0), Ta1);
+  ibfly(s, 6, 7, Tb0);
+  ctab(x.l1, cimg_lin(1), Tb1);
+  ibfly(s, 0, 2, Ta1);
+  ibfly(s, 1, 3, Ta1);
+  ctab(x.l2, cimg_lin(0), Ta2);
+  ibfly(s, 4, 6, Tb1);
+  ibfly(s, 5, 7, Tb1);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) ibfly(s, r, r + 4, Ta2);
+}
+
+// forward radix-8 pass at index off: stages B0+2, B0+1, B0 with table kinds
+// T2, T1, T0 (known per coset)
+template <int B0, typename T2, typename T1, typename T0>
+__device__ __forceinline__ void fpass(State &s, uint32_t base, uint32_t off) {
+  const XLanes x = xlanes<B0>(base);
+  const uint32_t u0 = cimg_lin(off >> (B0 + 1)), u1 = cimg_lin(off >> (B0 + 2)), u2 = cimg_lin(off >> (B0 + 3));
+  T2 Ta2;
+  T1 Ta1, Tb1;
+  T0 Ta0, Tb0;
+  ctab(x.l2, u2, Ta2);
+  ctab(x.l1, u1, Tb1);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) fbfly(s, r, r + 4, Ta2);
+  ctab(x.l1, u1 ^ cimg_lin(1), Ta1);
+  fbfly(s, 0, 2, Tb1);
+  fbfly(s, 1, 3, Tb1);
+  ctab(x.l0, u0, Tb0);
+  fbfly(s, 4, 6, Ta1);
+  fbfly(s, 5, 7, Ta1);
+  ctab(x.l0, u0 ^ cimg_lin(1), Ta0);
+  fbfly(s, 0, 1, Tb0);
+  ctab(x.l0, u0 ^ cimg_lin(2), Tb0);
+  fbfly(s, 2, 3, Ta0);
+  ctab(x.l0, u0 ^ cimg_lin(3), Ta0);
+  fbfly(s, 4, 5, Tb0);
+  fbfly(s, 6, 7, Ta0);
+}
+
+// wave-private exchange at the wave's region folded into the lane bases (bits
+// >= 12), the bases laundered so the cell addresses are formed here
+template <Layout FROM, Layout TO>
+__device__ __forceinline__ void xchg(State &s, XBase xb) {
+  asm volatile("" : "+v"(xb.a), "+v"(xb.b), "+v"(xb.c));
+#pragma unroll
+  for (int r = 0; r < 8; ++r) lds_st2(xcell<FROM>(xb, r), make_uint2(s.l[0][r], s.h[0][r]));
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const uint2 v = lds_ld2(xcell<TO>(xb, r));
+    s.l[0][r] = v.x;
+    s.h[0][r] = v.y;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ---- own-region staging: wave w stages its 16 pieces x 128 rows in its own
+// 4 KB region, 32 B per row (8 B per group g): row v, group g at 256-B block
+// v >> 3, 8-B slot ((v & 7) << 2 | g) ^ ((v >> 3) << 1) ^ (w << 2).  Layout-A
+// writes (rows 8 q + r, 32 lanes = 16 q x 2 g) and the store reads (16 lanes =
+// 8 waves x 2 group pairs of one row, 16 B each) are bank-conflict free.
+__host__ __device__ constexpr uint32_t soff(uint32_t v, uint32_t g, uint32_t w) {
+  return ((v >> 3) << 8) | (((((v & 7) << 2) | g) ^ ((v >> 3) << 1) ^ (w << 2)) & 31) << 3;
+}
+
+__device__ __forceinline__ void stage_own(const State &s, uint32_t q, uint32_t g, uint32_t wave) {
+  const uint32_t a = XCH0 + wave * XCH_BYTES + soff(8 * q, g, wave);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) lds_st2(a ^ soff(uint32_t(r), 0, 0), to_be(s.l[0][r], s.h[0][r]));
+}
+
+// all waves: rows [s0, s0 + 128) from the 8 regions -> shards.  Lane = (row in
+// 4, chunk c = pieces 8c..8c+7 = groups 2 (c & 1), + 1 of wave c >> 1); row v =
+// it * 32 + wave * 4 + lane / 16.  Fast path (uniform): 16-B aligned rows, the
+// whole tile inside the payload, all 128 rows below n_validators -- 4 streaming
+// 16-B stores per lane, 16 lanes per 256-B row segment.
+__device__ __forceinline__ bool store_fast(const uint8_t *SH, uint64_t sstride, uint32_t s0, int nv,
+                                           uint64_t piece0, uint64_t npieces) {
+  return ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0 && piece0 + TILE <= npieces &&
+         int(s0) + K <= nv;
+}
+
+template <typename Then>
+__device__ __forceinline__ void store_own(uint8_t *SH, uint64_t sstride, uint32_t s0, int nv,
+                                          uint64_t piece0, uint64_t npieces, uint32_t wave,
+                                          uint32_t lane, Then &&then) {
+  asm volatile("" : "+v"(lane));  // recomputed here, not kept live across the FFTs
+  const uint32_t c = lane & 15, cw = c >> 1;
+  const uint32_t v0 = wave * 4 + (lane >> 4);
+  const uint32_t ra = XCH0 + cw * XCH_BYTES + soff(v0, 2 * (c & 1), cw);  // 16-B aligned: groups 2h, 2h + 1
+  if (store_fast(SH, sstride, s0, nv, piece0, npieces)) {
+    uint8_t *dst = SH + uint64_t(s0 + v0) * sstride + 2 * (piece0 + 8 * c);
+    const uint64_t dstep = uint64_t(4 * WAVES) * sstride;
+#pragma unroll
+    for (int it = 0; it < K / (4 * WAVES); ++it) {  // soff is GF(2)-linear in v = it * 32 | v0
+      const v4u val = lds_r128(ra ^ soff(uint32_t(it) * 4 * WAVES, 0, 0));
+      __builtin_nontemporal_store(val, reinterpret_cast<v4u *>(dst + it * dstep));
+    }
+    then();
+    asm volatile("; store_own fast path end" ::: "memory");
+    return;
+  }
+  const uint64_t p = piece0 + 8 * c;
+  const bool wide = ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0;
+#pragma unroll
+  for (int it = 0; it < K / (4 * WAVES); ++it) {
+    const uint32_t v = uint32_t(it) * 4 * WAVES + v0;
+    const v4u val = lds_r128(ra ^ soff(uint32_t(it) * 4 * WAVES, 0, 0));
+    const uint32_t shard = s0 + v;
+    if (int(shard) >= nv) continue;
+    uint8_t *dst = SH + uint64_t(shard) * sstride + 2 * p;
+    if (p + 8 <= npieces) {
+      if (wide) {
+        *reinterpret_cast<v4u *>(dst) = val;
+      } else {
+        reinterpret_cast<uint2 *>(dst)[0] = make_uint2(val.x, val.y);
+        reinterpret_cast<uint2 *>(dst)[1] = make_uint2(val.z, val.w);
+      }
+    } else if (p < npieces) {
+      const uint32_t w[4] = {val.x, val.y, val.z, val.w};
+      for (uint64_t e = 0; e < npieces - p; ++e)
+        *reinterpret_cast<uint16_t *>(dst + 2 * e) = uint16_t(w[e >> 1] >> (16 * (e & 1)));
+    }
+  }
+  then();
+  asm volatile("; store_own slow path end" ::: "memory");
+}
+
+// 4 x 16 payload bytes (4 pieces, positions 8 q .. 8 q + 7) -> byte-planar
+// State (enc_k256w.hip to_state)
+__device__ __forceinline__ void to_state(const v4u (&d)[4], State &s) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t D0 = d[0][j], D1 = d[1][j], D2 = d[2][j], D3 = d[3][j];
+    const uint32_t t0 = vperm(D1, D0, 0x05010400u), t1 = vperm(D1, D0, 0x07030602u);
+    const uint32_t u0 = vperm(D3, D2, 0x05010400u), u1 = vperm(D3, D2, 0x07030602u);
+    s.h[0][2 * j] = vperm(u0, t0, 0x05040100u);
+    s.l[0][2 * j] = vperm(u0, t0, 0x07060302u);
+    s.h[0][2 * j + 1] = vperm(u1, t1, 0x05040100u);
+    s.l[0][2 * j + 1] = vperm(u1, t1, 0x07060302u);
+  }
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(THREADS, 4) encode_k128w(const uint8_t *__restrict__ payloads,
+                                                           uint64_t plen, uint64_t pstride,
+                                                           uint8_t *__restrict__ shards, uint64_t slen,
+                                                           uint64_t sstride, int nv, uint32_t batch,
+                                                           const uint8_t *__restrict__ cimg,
+                                                           uint32_t *__restrict__ tick) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const uint32_t tid0 = threadIdx.x;
+  auto *slot = reinterpret_cast<__attribute__((address_space(3))) volatile uint32_t *>(uintptr_t(SLOT));
+  if (tid0 == 0) *slot = tick ? atomicAdd(tick, 1u) : blockIdx.x;
+  {  // the compact image (32 KB), every load issued before the first store
+    constexpr int kPer = int(kCImgBytes / 16 / THREADS);
+    v4u v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) v[k] = reinterpret_cast<const v4u *>(cimg)[tid0 + k * THREADS];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) reinterpret_cast<v4u *>(lds)[tid0 + k * THREADS] = v[k];
+  }
+  __syncthreads();
+
+  const uint64_t npieces = slen / 2;
+  const uint32_t tiles_pp = uint32_t((npieces + TILE - 1) / TILE);
+  const uint32_t total = tiles_pp * batch;  // < 2^32 (launch_encode_k128w)
+  const uint32_t wave_s = __builtin_amdgcn_readfirstlane(tid0 >> 6);
+  const uint32_t J = uint32_t(nv - 1) / K;  // cosets 128 j, j = 1..J (nv <= n)
+  uint32_t cur = __builtin_amdgcn_readfirstlane(*slot);
+
+  // This lane's 4 x 16 payload bytes of tile (b, i): pieces i * TILE + 16 wave
+  // + 4 g + u (g = lane >> 4), bytes 16 q .. 16 q + 15 of each (q = lane & 15),
+  // zero past plen; issued in the previous tile's last coset.
+  v4u d[4];
+  State nxt;
+  const auto fetch = [&](uint64_t fb, uint64_t fi) __attribute__((always_inline)) {
+    const uint8_t *FP = payloads + fb * pstride;
+    const uint64_t pw = fi * TILE + WP * wave_s;  // this wave's first piece (uniform)
+    uint32_t ftid = tid0;
+    asm volatile("" : "+v"(ftid));
+    const uint32_t lane = ftid & 63, g = lane >> 4, q = lane & 15;
+    if ((pw + WP) * 2 * K <= plen) {  // the wave's 16 pieces inside the payload
+      const uint8_t *src = FP + (pw + 4 * g) * 2 * K + 16 * q;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d[u] = *reinterpret_cast<const v4u *>(src + u * 2 * K);
+    } else if (pw < npieces) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t off = (pw + 4 * g + u) * 2 * K + 16 * q;
+        uint32_t w[4] = {0, 0, 0, 0};
+        if (off + 16 <= plen) {
+          const v4u x = *reinterpret_cast<const v4u *>(FP + off);
+          w[0] = x.x;
+          w[1] = x.y;
+          w[2] = x.z;
+          w[3] = x.w;
+        } else {
+          for (uint64_t e = off; e < plen && e < off + 16; ++e)
+            w[(e - off) >> 2] |= uint32_t(FP[e]) << (8 * ((e - off) & 3));
+        }
+        d[u] = v4u{w[0], w[1], w[2], w[3]};
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d[u] = v4u{0, 0, 0, 0};
+    }
+  };
+  if (cur < total) {
+    fetch(cur / tiles_pp, cur % tiles_pp);
+    to_state(d, nxt);
+  }
+
+  while (cur < total) {
+    uint32_t tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const uint32_t lane = tid & 63, wave = tid >> 6;
+    // encode_k256w's lane roles: q5 = position bits 3..7 in layout A with i1
+    // as bit 7, inst = i0
+    const uint32_t q5 = lane & 31, i0 = lane >> 5;
+    const uint32_t reg0 = XCH0 + wave * XCH_BYTES;
+    XBase xb;
+    xb.a = reg0 | mswz(ulaneA(q5, i0));
+    xb.b = reg0 | mswz(ulaneB(q5, i0));
+    xb.c = reg0 | mswz(ulaneC(q5, i0));
+    const uint64_t b = cur / tiles_pp, piece0 = uint64_t(cur % tiles_pp) * TILE;
+    uint32_t taken = 0;
+    if (tid0 == 0) taken = tick ? atomicAdd(tick, 1u) : cur + gridDim.x;
+    uint32_t next = 0;
+    uint8_t *SH = shards + b * uint64_t(nv) * sstride;
+    const auto fetch_next = [&]() __attribute__((always_inline)) {
+      next = __builtin_amdgcn_readfirstlane(*slot);
+      fetch(next < total ? next / tiles_pp : 0, next < total ? next % tiles_pp : tiles_pp);
+    };
+    const auto rsync = [&]() __attribute__((always_inline)) { lds_barrier(); };
+    const auto store = [&](uint32_t s0, bool last) __attribute__((always_inline)) {
+      __builtin_amdgcn_s_setprio(1);
+      if (last)
+        store_own(SH, sstride, s0, nv, piece0, npieces, wave_s, lane,
+                  [&]() __attribute__((always_inline)) { to_state(d, nxt); });
+      else
+        store_own(SH, sstride, s0, nv, piece0, npieces, wave_s, lane, [] {});
+      __builtin_amdgcn_s_setprio(0);
+    };
+    const auto store_sys = [&]() __attribute__((always_inline)) {
+      __builtin_amdgcn_s_setprio(1);
+      store_own(SH, sstride, 0, nv, piece0, npieces, wave_s, lane, [&]() __attribute__((always_inline)) {
+        if (tid0 == 0) *slot = taken;
+      });
+      __builtin_amdgcn_s_setprio(0);
+    };
+
+    // a wave none of whose 16 pieces exist (the payload's last, partial tile)
+    // takes part only in the barriers and the row stores (uniform)
+    if (piece0 + WP * wave_s >= npieces) {
+      rsync();  // tile start
+      rsync();  // systematic rows staged
+      store_sys();
+      rsync();  // after IFFT pass A
+      for (uint32_t j = 1;; ++j) {
+        rsync();  // previous rows read out
+        if (j == J) {
+          fetch_next();
+          rsync();  // rows staged
+          store(K * j, true);
+          break;
+        }
+        rsync();  // rows staged
+        store(K * j, false);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      cur = next;
+      continue;
+    }
+
+    State s = nxt;
+    const uint32_t q = lane & 15, g = lane >> 4;
+    // ---- systematic shards 0..127 = the data symbols (poly_encoder.hpp:239)
+    rsync();  // the other waves are done reading the regions (last tile)
+    stage_own(s, q, g, wave);
+    rsync();
+    store_sys();
+    __builtin_amdgcn_sched_barrier(0);
+    {  // into tower coordinates
+      const TowerK tk = tower_k();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) s.l[0][r] = tower_lo(s.l[0][r], s.h[0][r], tk);
+    }
+
+    // ---- IFFT_128 (index 0): passes A (bits 0-2), B (3-5), stage 6 in C.
+    // Lane parts of the positions (i1 excluded): A 8 q, B posB(q5, 0) & 127
+    const uint32_t baseA = 8 * q, baseB = posB(q5, 0) & 127u;
+    ipass<0>(s, baseA);
+    rsync();  // systematic rows read out of the regions
+    xchg<LA, LB>(s, xb);
+    ipass<3>(s, baseB);
+    xchg<LB, LC>(s, xb);
+#pragma unroll
+    for (int r = 0; r < 8; r += 2) bxor(s, r, r + 1);  // stage 6, x = 0 (additive_fft.hpp:110-112)
+    State coef = s;
+
+    // ---- FFT_128 at each coset 128 j (encodeLow, poly_encoder.hpp:229-237).
+    // Kinds (x = (pos + off) >> (m + 1)): stage 0 subfield (j = 1), F9 (2, 3),
+    // general (4..7); stage 1 subfield (j <= 3), F9 above; stages 2-6 subfield.
+    const auto coset = [&](auto t1, auto t0, const uint32_t j) __attribute__((always_inline)) {
+      using T1 = decltype(t1);
+      using T0 = decltype(t0);
+      const uint32_t off = K * j;
+      uint32_t bA = baseA, bB = baseB;
+      asm volatile("" : "+v"(bA), "+v"(bB));  // table addresses formed per coset, not hoisted
+#pragma unroll
+      for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(coef.l[0][r]), "+v"(coef.h[0][r]));
+      {  // stage 6, x = off >> 7, from the coefficients
+        SubTab T6;
+        ctab(0u, cimg_lin(off >> 7), T6);
+#pragma unroll
+        for (int r = 0; r < 8; r += 2) fbfly_from(s, coef, r, r + 1, T6);
+      }
+      rsync();  // previous coset's rows read out
+      xchg<LC, LB>(s, xb);
+      fpass<3, SubTab, SubTab, SubTab>(s, bB, off);
+      xchg<LB, LA>(s, xb);
+      fpass<0, SubTab, T1, T0>(s, bA, off);
+      {  // back to symbol coordinates
+        const TowerK tk = tower_k();
+#pragma unroll
+        for (int r = 0; r < 8; ++r) s.l[0][r] = tower_lo(s.l[0][r], s.h[0][r], tk);
+      }
+      stage_own(s, q, g, wave);
+    };
+    // the cosets in a loop (three bodies, by table kinds); the last one leaves
+    // it, so the next tile's payload (d, nxt) is live in that one only
+    for (uint32_t j = 1;; ++j) {
+      if (j == 1) coset(SubTab(), SubTab(), j);
+      else if (j <= 3) coset(SubTab(), F9Tab(), j);
+      else coset(F9Tab(), Tab(), j);
+      if (j == J) {
+        fetch_next();  // coef and s are dead here
+        rsync();       // rows staged
+        store(K * j, true);
+        break;
+      }
+      rsync();  // rows staged
+      store(K * j, false);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    cur = next;
+  }
+}
+
+bool k128w_applicable(const CodeParams &p) { return p.k == 128 && (p.n == 512 || p.n == 1024); }
+
+size_t k128w_scratch_bytes(const CodeParams &p) { return k128w_applicable(p) ? 256 : 0; }
+
+hipError_t launch_encode_k128w(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
+                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
+                               size_t sstride, void *scratch, hipStream_t s) {
+  int cus = 0;
+  if (!t.cimg) return hipErrorInvalidValue;
+  if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&encode_k128w), LDS_BYTES, &cus);
+      e != hipSuccess)
+    return e;
+  if (!k128w_applicable(p) || p.nv <= uint32_t(K) || p.nv > p.n) return hipErrorInvalidValue;
+  const size_t sl = shard_len(p.k, plen);
+  const size_t tiles = (sl / 2 + TILE - 1) / TILE * batch;
+  if (tiles >= (size_t(1) << 32) - size_t(4) * cus) return hipErrorInvalidValue;
+  uint32_t *tick = static_cast<uint32_t *>(scratch);  // none: the static schedule
+  if (tick)
+    if (const hipError_t e = launch_zero_counters(tick, sizeof(uint32_t), s); e != hipSuccess) return e;
+  const size_t slots = 2 * size_t(cus);  // two workgroups per CU
+  const unsigned grid = unsigned(tiles < slots ? tiles : slots);
+  hipLaunchKernelGGL(encode_k128w, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads, uint64_t(plen),
+                     uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride), int(p.nv),
+                     uint32_t(batch), t.cimg, tick);
+  return hipGetLastError();
+}
+
+}  // namespace ecamd

@@ -100,3 +100,14 @@ def test_enc_k512w_fast_store_count_no_spills(tmp_path):
     body = text[text.index("encode_k512w"):]
     body = body[:body.index("s_endpgm")]
     assert "scratch_" not in body
+
+
+def test_enc_k128w_fast_store_count_no_spills(tmp_path):
+    # enc_k128w.hip: store_own's fast path, 4 stores per lane (the compiler's
+    # own vmcnt(4) before the next tile's transposes counts them); no spills
+    text = _asm("enc_k128w.hip", tmp_path)
+    blocks = _nt_store_blocks(text, "encode_k128w")
+    assert blocks and all(c == 4 for c in blocks), blocks
+    body = text[text.index("encode_k128w"):]
+    body = body[:body.index("s_endpgm")]
+    assert "scratch_" not in body

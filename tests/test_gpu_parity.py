@@ -232,6 +232,33 @@ def test_encode_k512w_vs_oracle(oracle, nv, plen, batch, pad):
         assert (got[b, :, sl:] == 0x5C).all()  # nothing past the shard length
 
 
+@pytest.mark.parametrize("nv,plen,batch,pad", [
+    (382, 70001, 3, 64), (383, 1, 2, 16), (384, 32768, 2, 16), (512, 32769, 3, 8),
+    (513, 40001, 2, 64), (600, 255, 2, 16), (640, 3 * 32768, 2, 64), (641, 30001, 2, 8),
+    (700, 257, 3, 64), (765, 100001, 3, 16), (765, 1_000_000, 2, 64)])
+def test_encode_k128w_vs_oracle(oracle, nv, plen, batch, pad):
+    """enc_k128w.hip (k = 128, n = 512 / 1024): the first and last
+    n_validators of each coset count (J = 2..5 cosets, the last partly below
+    n_validators), payloads of one piece, of whole and partial 128-piece tiles
+    (waves with no pieces), 8 / 16 / 64-byte row pitches, against the
+    reference encoder."""
+    import torch
+    n, k, _ = E.code_params(nv)
+    assert k == 128
+    sl = E.shard_len(nv, plen)
+    ss = (sl + pad - 1) // pad * pad
+    pays = [synth.payload(nv * 5 + b, plen) for b in range(batch)]
+    d_pay = torch.from_numpy(np.stack(pays)).cuda()
+    d_sh = torch.full((batch, nv, ss), 0x5C, dtype=torch.uint8, device="cuda")
+    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+    torch.cuda.synchronize()
+    got = d_sh.cpu().numpy()
+    for b in range(batch):
+        want = oracle.encode(nv, pays[b].tobytes())
+        assert b"".join(want) == got[b, :, :sl].tobytes(), (nv, plen, b)
+        assert (got[b, :, sl:] == 0x5C).all()
+
+
 def test_batch_config2_roundtrip():
     """BASELINE config 2 shape (n_validators=1024, 1 MB payloads, 342 random shards):
     size-independent round trip + batch-vs-single equality on a batch of 8."""
