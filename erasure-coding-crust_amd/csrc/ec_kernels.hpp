@@ -201,13 +201,13 @@ hipError_t launch_encode_k512w(const CodeParams &p, const DevTables &t, const ui
                                size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                                size_t sstride, void *scratch, hipStream_t s);
 
-// k = 128, n = 512 / 1024 (enc_k128w.hip): the same model on the compact
-// image alone; scratch (nullable) the tile counter, k128w_scratch_bytes
-bool k128w_applicable(const CodeParams &p);
-size_t k128w_scratch_bytes(const CodeParams &p);
-hipError_t launch_encode_k128w(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
-                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
-                               size_t sstride, void *scratch, hipStream_t s);
+// k = 16 .. 128, n <= 8 k (enc_kw.hip): the same model on the compact image
+// alone; scratch (nullable) the tile counter, kw_scratch_bytes
+bool kw_applicable(const CodeParams &p);
+size_t kw_scratch_bytes(const CodeParams &p);
+hipError_t launch_encode_kw(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
+                            size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
+                            size_t sstride, void *scratch, hipStream_t s);
 
 // register-blocked encode for k = 16 .. 512, n <= 4096 (enc_gen.hip)
 bool encgen_applicable(const CodeParams &p);

@@ -1,21 +1,24 @@
-// enc_k128w.hip — encode for k = 128, n = 512 / 1024 (n_validators 382..765,
-// the Polkadot validator counts of today), two 8-wave workgroups per CU.
+// enc_kw.hip — encode for k = 2^M = 16, 32, 64, 128 (n <= 8 k: n_validators
+// 46..765, the Polkadot validator counts of today among them), two 8-wave
+// workgroups per CU.
 //
-// encode_k256w's model (enc_k256w.hip) at k = 128: per piece
-// (256 payload bytes = 128 symbols) IFFT_128 at index 0, then FFT_128 at each
-// coset 128 j below n_validators (encodeLow, poly_encoder.hpp:217-240), radix-8
+// encode_k256w's model (enc_k256w.hip) at small k: per piece
+// (2 k payload bytes = k symbols) IFFT_k at index 0, then FFT_k at each coset
+// k j below n_validators (encodeLow, poly_encoder.hpp:217-240), radix-8
 // register passes in tower coordinates, wave-private LDS exchanges.  A wave
-// holds four byte-planar groups of 4 pieces (16 pieces), each group's 128
-// positions over 16 lanes x 8 registers.  The instance bits are i1 = lane bit 4
-// and i0 = lane bit 5; read as position bit 7 and encode_k256w's instance bit,
-// the layouts A / B / C and their exchanges are encode_k256w's, so:
-//  * layout A: registers p0..p2, layout B: p3..p5, layout C: p6 (register bit
-//    0), i1 (bit 1), p5 (bit 2) -- stage 6 runs in C on register pairs, its
-//    element x = (pos + off) >> 7 uniform;
-//  * every element is x < 512 (stage 0 at the last coset 896: < 512), so the
-//    32 KB compact image holds all tables: LDS 64 KB per workgroup;
-//  * the tile is 128 pieces (8 waves x 16), each shard row a 256-B segment,
-//    stored as 16 B per lane (two groups of one wave).
+// holds NG = 512 / k byte-planar groups of 4 pieces; a group's k positions lie
+// over k / 8 lanes x 8 registers, the group index in the lane bits above.
+// Read as position bits M..7 and encode_k256w's instance bit, the group bits
+// make every layout and exchange encode_k256w's:
+//  * layout A: registers p0..p2 (lane part 8 q, q = lane & (k/8 - 1));
+//  * layout B: registers p3..p5 as far as they are positions (M = 4: p3 only,
+//    M = 5: p3, p4), lanes p0..p2 and p6; for M <= 6 its elements are
+//    wave-uniform;
+//  * M = 7: stage 6 in layout C's register bit 0;
+//  * every element is x < 2^(M+2) <= 512: the 32 KB compact image holds all
+//    tables, LDS 64 KB per workgroup;
+//  * tiles of 8 NG pieces per wave (32 KB of payload), shard-row segments of
+//    64 NG bytes stored as 16 B per lane (two groups of one wave).
 #include <hip/hip_runtime.h>
 
 #include "ec_device.hpp"
@@ -26,11 +29,8 @@
 namespace ecamd {
 namespace {
 
-constexpr int K = 128;
 constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
-constexpr int WP = 16;                       // pieces per wave
-constexpr int TILE = WP * WAVES;             // pieces per tile
 constexpr uint32_t XCH0 = kCImgBytes;        // the wave regions follow the tables
 constexpr uint32_t XCH_BYTES = 4096;
 constexpr uint32_t SLOT = XCH0 + WAVES * XCH_BYTES;  // the next tile's index
@@ -38,6 +38,18 @@ constexpr int LDS_BYTES = int(SLOT + 16);
 static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
 static_assert(XCH0 % (2 * XCH_BYTES) == 0, "XOR-addressed regions");
 static_assert(kCImgBytes % (16 * THREADS) == 0, "whole image chunks per thread");
+
+template <int M>
+struct Geo {
+  static constexpr uint32_t K = 1u << M;
+  static constexpr int NG = 512 >> M;          // byte-planar groups per wave
+  static constexpr int WP = 4 * NG;            // pieces per wave
+  static constexpr int TILE = WP * WAVES;      // pieces per tile (32 KB of payload)
+  static constexpr int RC = 4 * NG;            // 16-B chunks per shard-row segment
+  static constexpr int RPI = 512 / RC;         // rows per store iteration (all waves), 0 if < 1
+  static constexpr uint32_t QM = (1u << (M - 3)) - 1;  // lane mask of the layout-A position part
+  static_assert(M >= 4 && M <= 7, "k = 16 .. 128");
+};
 
 struct XLanes {
   uint32_t l0, l1, l2;
@@ -99,6 +111,79 @@ __device__ __forceinline__ void fpass(State &s, uint32_t base, uint32_t off) {
   fbfly(s, 6, 7, Ta0);
 }
 
+// ---- layout B for M <= 6: registers p3, p4, p5 as far as they are positions
+// (the others group bits), no lane part: every element is x = (register
+// position bits above m) | (off >> (m + 1)), wave-uniform.  Stage 3 pairs
+// registers (2 rr, 2 rr + 1), rr = (p4, p5); stage 4 (r, r + 2), block p5;
+// stage 5 (r, r + 4).
+template <int M>
+constexpr uint32_t bmask3() { return (M > 4 ? 1u : 0u) | (M > 5 ? 2u : 0u); }
+template <int M>
+constexpr uint32_t bmask4() { return M > 5 ? 1u : 0u; }
+
+// IFFT stages 3 .. M - 1 at index 0 (x = 0: b ^= a only, additive_fft.hpp:110-112)
+template <int M>
+__device__ __forceinline__ void ipassB_u(State &s) {
+  SubTab T1, T2, T3;
+  ctab(0u, cimg_lin(1), T1);
+  if constexpr (M > 5) {
+    ctab(0u, cimg_lin(2), T2);
+    ctab(0u, cimg_lin(3), T3);
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const uint32_t x = uint32_t(rr) & bmask3<M>();
+    if (x == 0) bxor(s, 2 * rr, 2 * rr + 1);
+    else if (x == 1) ibfly(s, 2 * rr, 2 * rr + 1, T1);
+    else if (x == 2) ibfly(s, 2 * rr, 2 * rr + 1, T2);
+    else ibfly(s, 2 * rr, 2 * rr + 1, T3);
+  }
+  if constexpr (M > 4) {
+#pragma unroll
+    for (int r : {0, 1, 4, 5}) {
+      if (((uint32_t(r) >> 2) & bmask4<M>()) == 0) bxor(s, r, r + 2);
+      else ibfly(s, r, r + 2, T1);
+    }
+  }
+  if constexpr (M > 5) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bxor(s, r, r + 4);
+  }
+}
+
+// FFT stages M - 1 .. 3 at index off, the first one reading the IFFT
+// coefficients c
+template <int M>
+__device__ __forceinline__ void fpassB_u(State &s, const State &c, uint32_t off) {
+  if constexpr (M > 5) {  // stage 5, x = off >> 6
+    SubTab T;
+    ctab(0u, cimg_lin(off >> 6), T);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) fbfly_from(s, c, r, r + 4, T);
+  }
+  if constexpr (M > 4) {  // stage 4, x = off >> 5 | p5
+    SubTab Ta, Tb;
+    ctab(0u, cimg_lin(off >> 5), Ta);
+    ctab(0u, cimg_lin(off >> 5) ^ cimg_lin(bmask4<M>()), Tb);
+#pragma unroll
+    for (int r : {0, 1, 4, 5}) {
+      const SubTab &T = (uint32_t(r) >> 2) & bmask4<M>() ? Tb : Ta;
+      if constexpr (M == 5) fbfly_from(s, c, r, r + 2, T);
+      else fbfly(s, r, r + 2, T);
+    }
+  }
+  {  // stage 3, x = off >> 4 | (p4, p5)
+    SubTab T[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) ctab(0u, cimg_lin(off >> 4) ^ cimg_lin(uint32_t(rr) & bmask3<M>()), T[rr]);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      if constexpr (M == 4) fbfly_from(s, c, 2 * rr, 2 * rr + 1, T[rr]);
+      else fbfly(s, 2 * rr, 2 * rr + 1, T[rr]);
+    }
+  }
+}
+
 // wave-private exchange at the wave's region folded into the lane bases (bits
 // >= 12), the bases laundered so the cell addresses are formed here
 template <Layout FROM, Layout TO>
@@ -118,46 +203,52 @@ __device__ __forceinline__ void xchg(State &s, XBase xb) {
   __builtin_amdgcn_wave_barrier();
 }
 
-// ---- own-region staging: wave w stages its 16 pieces x 128 rows in its own
-// 4 KB region, 32 B per row (8 B per group g): row v, group g at 256-B block
-// v >> 3, 8-B slot ((v & 7) << 2 | g) ^ ((v >> 3) << 1) ^ (w << 2).  Layout-A
-// writes (rows 8 q + r, 32 lanes = 16 q x 2 g) and the store reads (16 lanes =
-// 8 waves x 2 group pairs of one row, 16 B each) are bank-conflict free.
+// ---- own-region staging: wave w stages its NG groups x k rows in its own
+// 4 KB region, 8 B per (row v, group g) at slot (v NG + g) ^ (v >> 3) << (8 -
+// M) ^ ((w << (9 - M)) & 31).  Layout-A writes (rows 8 q + r; 32 lanes = the
+// q and the low group bits) and the store reads (16 lanes x 16 B = group pairs
+// (2h, 2h + 1) of one row across waves) hit distinct banks.
+template <int M>
 __host__ __device__ constexpr uint32_t soff(uint32_t v, uint32_t g, uint32_t w) {
-  return ((v >> 3) << 8) | (((((v & 7) << 2) | g) ^ ((v >> 3) << 1) ^ (w << 2)) & 31) << 3;
+  return (((v << (9 - M)) | g) ^ ((v >> 3) << (8 - M)) ^ ((w << (9 - M)) & 31u)) << 3;
 }
 
+template <int M>
 __device__ __forceinline__ void stage_own(const State &s, uint32_t q, uint32_t g, uint32_t wave) {
-  const uint32_t a = XCH0 + wave * XCH_BYTES + soff(8 * q, g, wave);
+  const uint32_t a = XCH0 + wave * XCH_BYTES + soff<M>(8 * q, g, wave);
 #pragma unroll
-  for (int r = 0; r < 8; ++r) lds_st2(a ^ soff(uint32_t(r), 0, 0), to_be(s.l[0][r], s.h[0][r]));
+  for (int r = 0; r < 8; ++r) lds_st2(a ^ soff<M>(uint32_t(r), 0, 0), to_be(s.l[0][r], s.h[0][r]));
 }
 
-// all waves: rows [s0, s0 + 128) from the 8 regions -> shards.  Lane = (row in
-// 4, chunk c = pieces 8c..8c+7 = groups 2 (c & 1), + 1 of wave c >> 1); row v =
-// it * 32 + wave * 4 + lane / 16.  Fast path (uniform): 16-B aligned rows, the
-// whole tile inside the payload, all 128 rows below n_validators -- 4 streaming
-// 16-B stores per lane, 16 lanes per 256-B row segment.
+// all waves: rows [s0, s0 + k) from the 8 regions -> shards.  Chunk G = it *
+// 512 + thread: row v = G / RC, chunk c = G % RC (16 B = pieces 8c..8c+7 =
+// groups 2h, 2h + 1 of wave c / (NG / 2)).  Fast path (uniform): 16-B aligned
+// rows, the whole tile inside the payload, all k rows below n_validators -- 4
+// streaming 16-B stores per lane.
+template <int M>
 __device__ __forceinline__ bool store_fast(const uint8_t *SH, uint64_t sstride, uint32_t s0, int nv,
                                            uint64_t piece0, uint64_t npieces) {
-  return ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0 && piece0 + TILE <= npieces &&
-         int(s0) + K <= nv;
+  return ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0 && piece0 + Geo<M>::TILE <= npieces &&
+         int(s0) + int(Geo<M>::K) <= nv;
 }
 
-template <typename Then>
+template <int M, typename Then>
 __device__ __forceinline__ void store_own(uint8_t *SH, uint64_t sstride, uint32_t s0, int nv,
                                           uint64_t piece0, uint64_t npieces, uint32_t wave,
                                           uint32_t lane, Then &&then) {
+  using G = Geo<M>;
   asm volatile("" : "+v"(lane));  // recomputed here, not kept live across the FFTs
-  const uint32_t c = lane & 15, cw = c >> 1;
-  const uint32_t v0 = wave * 4 + (lane >> 4);
-  const uint32_t ra = XCH0 + cw * XCH_BYTES + soff(v0, 2 * (c & 1), cw);  // 16-B aligned: groups 2h, 2h + 1
-  if (store_fast(SH, sstride, s0, nv, piece0, npieces)) {
+  const uint32_t t = wave * 64 + lane;
+  const uint32_t v0 = t / G::RC, c = t % G::RC;  // it = 0
+  const uint32_t cw = c / (G::NG / 2), h = c % (G::NG / 2);
+  const uint32_t ra = XCH0 + cw * XCH_BYTES + soff<M>(v0, 2 * h, cw);  // 16-B aligned: groups 2h, 2h + 1
+  constexpr uint32_t VSTEP = 512 / G::RC;  // rows per iteration
+  if (store_fast<M>(SH, sstride, s0, nv, piece0, npieces)) {
     uint8_t *dst = SH + uint64_t(s0 + v0) * sstride + 2 * (piece0 + 8 * c);
-    const uint64_t dstep = uint64_t(4 * WAVES) * sstride;
+    const uint64_t dstep = uint64_t(VSTEP) * sstride;
 #pragma unroll
-    for (int it = 0; it < K / (4 * WAVES); ++it) {  // soff is GF(2)-linear in v = it * 32 | v0
-      const v4u val = lds_r128(ra ^ soff(uint32_t(it) * 4 * WAVES, 0, 0));
+    for (int it = 0; it < 4; ++it) {  // soff is GF(2)-linear in v = it * VSTEP | v0
+      const v4u val = lds_r128(ra ^ soff<M>(uint32_t(it) * VSTEP, 0, 0));
       __builtin_nontemporal_store(val, reinterpret_cast<v4u *>(dst + it * dstep));
     }
     then();
@@ -167,9 +258,9 @@ __device__ __forceinline__ void store_own(uint8_t *SH, uint64_t sstride, uint32_
   const uint64_t p = piece0 + 8 * c;
   const bool wide = ((sstride | reinterpret_cast<uintptr_t>(SH)) & 15) == 0;
 #pragma unroll
-  for (int it = 0; it < K / (4 * WAVES); ++it) {
-    const uint32_t v = uint32_t(it) * 4 * WAVES + v0;
-    const v4u val = lds_r128(ra ^ soff(uint32_t(it) * 4 * WAVES, 0, 0));
+  for (int it = 0; it < 4; ++it) {
+    const uint32_t v = uint32_t(it) * VSTEP + v0;
+    const v4u val = lds_r128(ra ^ soff<M>(uint32_t(it) * VSTEP, 0, 0));
     const uint32_t shard = s0 + v;
     if (int(shard) >= nv) continue;
     uint8_t *dst = SH + uint64_t(shard) * sstride + 2 * p;
@@ -207,12 +298,15 @@ __device__ __forceinline__ void to_state(const v4u (&d)[4], State &s) {
 
 }  // namespace
 
-__global__ void __launch_bounds__(THREADS, 4) encode_k128w(const uint8_t *__restrict__ payloads,
-                                                           uint64_t plen, uint64_t pstride,
-                                                           uint8_t *__restrict__ shards, uint64_t slen,
-                                                           uint64_t sstride, int nv, uint32_t batch,
-                                                           const uint8_t *__restrict__ cimg,
-                                                           uint32_t *__restrict__ tick) {
+template <int M>
+__global__ void __launch_bounds__(THREADS, 4) encode_kw(const uint8_t *__restrict__ payloads,
+                                                        uint64_t plen, uint64_t pstride,
+                                                        uint8_t *__restrict__ shards, uint64_t slen,
+                                                        uint64_t sstride, int nv, uint32_t batch,
+                                                        const uint8_t *__restrict__ cimg,
+                                                        uint32_t *__restrict__ tick) {
+  using G = Geo<M>;
+  constexpr uint32_t K = G::K;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid0 = threadIdx.x;
   auto *slot = reinterpret_cast<__attribute__((address_space(3))) volatile uint32_t *>(uintptr_t(SLOT));
@@ -228,24 +322,24 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k128w(const uint8_t *__rest
   __syncthreads();
 
   const uint64_t npieces = slen / 2;
-  const uint32_t tiles_pp = uint32_t((npieces + TILE - 1) / TILE);
-  const uint32_t total = tiles_pp * batch;  // < 2^32 (launch_encode_k128w)
+  const uint32_t tiles_pp = uint32_t((npieces + G::TILE - 1) / G::TILE);
+  const uint32_t total = tiles_pp * batch;  // < 2^32 (launch_encode_kw)
   const uint32_t wave_s = __builtin_amdgcn_readfirstlane(tid0 >> 6);
-  const uint32_t J = uint32_t(nv - 1) / K;  // cosets 128 j, j = 1..J (nv <= n)
+  const uint32_t J = uint32_t(nv - 1) / K;  // cosets k j, j = 1..J <= 7 (nv <= n <= 8 k)
   uint32_t cur = __builtin_amdgcn_readfirstlane(*slot);
 
-  // This lane's 4 x 16 payload bytes of tile (b, i): pieces i * TILE + 16 wave
-  // + 4 g + u (g = lane >> 4), bytes 16 q .. 16 q + 15 of each (q = lane & 15),
-  // zero past plen; issued in the previous tile's last coset.
+  // This lane's 4 x 16 payload bytes of tile (b, i): pieces i * TILE + WP wave
+  // + 4 g + u (g = lane >> (M - 3)), bytes 16 q .. 16 q + 15 of each (q = lane
+  // & QM), zero past plen; issued in the previous tile's last coset.
   v4u d[4];
   State nxt;
   const auto fetch = [&](uint64_t fb, uint64_t fi) __attribute__((always_inline)) {
     const uint8_t *FP = payloads + fb * pstride;
-    const uint64_t pw = fi * TILE + WP * wave_s;  // this wave's first piece (uniform)
+    const uint64_t pw = fi * G::TILE + G::WP * wave_s;  // this wave's first piece (uniform)
     uint32_t ftid = tid0;
     asm volatile("" : "+v"(ftid));
-    const uint32_t lane = ftid & 63, g = lane >> 4, q = lane & 15;
-    if ((pw + WP) * 2 * K <= plen) {  // the wave's 16 pieces inside the payload
+    const uint32_t lane = ftid & 63, g = lane >> (M - 3), q = lane & G::QM;
+    if ((pw + G::WP) * 2 * K <= plen) {  // the wave's pieces inside the payload
       const uint8_t *src = FP + (pw + 4 * g) * 2 * K + 16 * q;
 #pragma unroll
       for (int u = 0; u < 4; ++u) d[u] = *reinterpret_cast<const v4u *>(src + u * 2 * K);
@@ -280,15 +374,15 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k128w(const uint8_t *__rest
     uint32_t tid = tid0;
     asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63, wave = tid >> 6;
-    // encode_k256w's lane roles: q5 = position bits 3..7 in layout A with i1
-    // as bit 7, inst = i0
+    // encode_k256w's lane roles: q5 = position bits 3..7 in layout A (the
+    // group bits above p(M-1) read as positions), inst = lane bit 5
     const uint32_t q5 = lane & 31, i0 = lane >> 5;
     const uint32_t reg0 = XCH0 + wave * XCH_BYTES;
     XBase xb;
     xb.a = reg0 | mswz(ulaneA(q5, i0));
     xb.b = reg0 | mswz(ulaneB(q5, i0));
     xb.c = reg0 | mswz(ulaneC(q5, i0));
-    const uint64_t b = cur / tiles_pp, piece0 = uint64_t(cur % tiles_pp) * TILE;
+    const uint64_t b = cur / tiles_pp, piece0 = uint64_t(cur % tiles_pp) * G::TILE;
     uint32_t taken = 0;
     if (tid0 == 0) taken = tick ? atomicAdd(tick, 1u) : cur + gridDim.x;
     uint32_t next = 0;
@@ -301,23 +395,23 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k128w(const uint8_t *__rest
     const auto store = [&](uint32_t s0, bool last) __attribute__((always_inline)) {
       __builtin_amdgcn_s_setprio(1);
       if (last)
-        store_own(SH, sstride, s0, nv, piece0, npieces, wave_s, lane,
-                  [&]() __attribute__((always_inline)) { to_state(d, nxt); });
+        store_own<M>(SH, sstride, s0, nv, piece0, npieces, wave_s, lane,
+                     [&]() __attribute__((always_inline)) { to_state(d, nxt); });
       else
-        store_own(SH, sstride, s0, nv, piece0, npieces, wave_s, lane, [] {});
+        store_own<M>(SH, sstride, s0, nv, piece0, npieces, wave_s, lane, [] {});
       __builtin_amdgcn_s_setprio(0);
     };
     const auto store_sys = [&]() __attribute__((always_inline)) {
       __builtin_amdgcn_s_setprio(1);
-      store_own(SH, sstride, 0, nv, piece0, npieces, wave_s, lane, [&]() __attribute__((always_inline)) {
+      store_own<M>(SH, sstride, 0, nv, piece0, npieces, wave_s, lane, [&]() __attribute__((always_inline)) {
         if (tid0 == 0) *slot = taken;
       });
       __builtin_amdgcn_s_setprio(0);
     };
 
-    // a wave none of whose 16 pieces exist (the payload's last, partial tile)
+    // a wave none of whose pieces exist (the payload's last, partial tile)
     // takes part only in the barriers and the row stores (uniform)
-    if (piece0 + WP * wave_s >= npieces) {
+    if (piece0 + G::WP * wave_s >= npieces) {
       rsync();  // tile start
       rsync();  // systematic rows staged
       store_sys();
@@ -339,10 +433,10 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k128w(const uint8_t *__rest
     }
 
     State s = nxt;
-    const uint32_t q = lane & 15, g = lane >> 4;
-    // ---- systematic shards 0..127 = the data symbols (poly_encoder.hpp:239)
+    const uint32_t q = lane & G::QM, g = lane >> (M - 3);
+    // ---- systematic shards 0..k-1 = the data symbols (poly_encoder.hpp:239)
     rsync();  // the other waves are done reading the regions (last tile)
-    stage_own(s, q, g, wave);
+    stage_own<M>(s, q, g, wave);
     rsync();
     store_sys();
     __builtin_amdgcn_sched_barrier(0);
@@ -352,21 +446,27 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k128w(const uint8_t *__rest
       for (int r = 0; r < 8; ++r) s.l[0][r] = tower_lo(s.l[0][r], s.h[0][r], tk);
     }
 
-    // ---- IFFT_128 (index 0): passes A (bits 0-2), B (3-5), stage 6 in C.
-    // Lane parts of the positions (i1 excluded): A 8 q, B posB(q5, 0) & 127
+    // ---- IFFT_k (index 0): pass A (bits 0-2), then pass B (bits 3..M-1;
+    // M = 7: 3-5, then stage 6 in layout C).  Lane parts of the positions
+    // (group bits excluded): A 8 q, B (M = 7) posB(q5, 0) & 127
     const uint32_t baseA = 8 * q, baseB = posB(q5, 0) & 127u;
     ipass<0>(s, baseA);
     rsync();  // systematic rows read out of the regions
     xchg<LA, LB>(s, xb);
-    ipass<3>(s, baseB);
-    xchg<LB, LC>(s, xb);
+    if constexpr (M == 7) {
+      ipass<3>(s, baseB);
+      xchg<LB, LC>(s, xb);
 #pragma unroll
-    for (int r = 0; r < 8; r += 2) bxor(s, r, r + 1);  // stage 6, x = 0 (additive_fft.hpp:110-112)
+      for (int r = 0; r < 8; r += 2) bxor(s, r, r + 1);  // stage 6, x = 0 (additive_fft.hpp:110-112)
+    } else {
+      ipassB_u<M>(s);
+    }
     State coef = s;
 
-    // ---- FFT_128 at each coset 128 j (encodeLow, poly_encoder.hpp:229-237).
-    // Kinds (x = (pos + off) >> (m + 1)): stage 0 subfield (j = 1), F9 (2, 3),
-    // general (4..7); stage 1 subfield (j <= 3), F9 above; stages 2-6 subfield.
+    // ---- FFT_k at each coset k j (encodeLow, poly_encoder.hpp:229-237).
+    // Kinds (x = (pos + off) >> (m + 1)): M = 7: stage 0 subfield (j = 1), F9
+    // (2, 3), general (4..7), stage 1 subfield (j <= 3), F9 above; M = 6:
+    // stage 0 subfield (j <= 3), F9 above; everything else subfield.
     const auto coset = [&](auto t1, auto t0, const uint32_t j) __attribute__((always_inline)) {
       using T1 = decltype(t1);
       using T0 = decltype(t0);
@@ -375,15 +475,20 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k128w(const uint8_t *__rest
       asm volatile("" : "+v"(bA), "+v"(bB));  // table addresses formed per coset, not hoisted
 #pragma unroll
       for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(coef.l[0][r]), "+v"(coef.h[0][r]));
-      {  // stage 6, x = off >> 7, from the coefficients
-        SubTab T6;
-        ctab(0u, cimg_lin(off >> 7), T6);
+      if constexpr (M == 7) {
+        {  // stage 6, x = off >> 7, from the coefficients
+          SubTab T6;
+          ctab(0u, cimg_lin(off >> 7), T6);
 #pragma unroll
-        for (int r = 0; r < 8; r += 2) fbfly_from(s, coef, r, r + 1, T6);
+          for (int r = 0; r < 8; r += 2) fbfly_from(s, coef, r, r + 1, T6);
+        }
+        rsync();  // previous coset's rows read out
+        xchg<LC, LB>(s, xb);
+        fpass<3, SubTab, SubTab, SubTab>(s, bB, off);
+      } else {
+        fpassB_u<M>(s, coef, off);
+        rsync();  // previous coset's rows read out
       }
-      rsync();  // previous coset's rows read out
-      xchg<LC, LB>(s, xb);
-      fpass<3, SubTab, SubTab, SubTab>(s, bB, off);
       xchg<LB, LA>(s, xb);
       fpass<0, SubTab, T1, T0>(s, bA, off);
       {  // back to symbol coordinates
@@ -391,14 +496,21 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k128w(const uint8_t *__rest
 #pragma unroll
         for (int r = 0; r < 8; ++r) s.l[0][r] = tower_lo(s.l[0][r], s.h[0][r], tk);
       }
-      stage_own(s, q, g, wave);
+      stage_own<M>(s, q, g, wave);
     };
-    // the cosets in a loop (three bodies, by table kinds); the last one leaves
+    // the cosets in a loop (a body per table-kind class); the last one leaves
     // it, so the next tile's payload (d, nxt) is live in that one only
     for (uint32_t j = 1;; ++j) {
-      if (j == 1) coset(SubTab(), SubTab(), j);
-      else if (j <= 3) coset(SubTab(), F9Tab(), j);
-      else coset(F9Tab(), Tab(), j);
+      if constexpr (M == 7) {
+        if (j == 1) coset(SubTab(), SubTab(), j);
+        else if (j <= 3) coset(SubTab(), F9Tab(), j);
+        else coset(F9Tab(), Tab(), j);
+      } else if constexpr (M == 6) {
+        if (j <= 3) coset(SubTab(), SubTab(), j);
+        else coset(SubTab(), F9Tab(), j);
+      } else {
+        coset(SubTab(), SubTab(), j);
+      }
       if (j == J) {
         fetch_next();  // coef and s are dead here
         rsync();       // rows staged
@@ -413,31 +525,44 @@ __global__ void __launch_bounds__(THREADS, 4) encode_k128w(const uint8_t *__rest
   }
 }
 
-bool k128w_applicable(const CodeParams &p) { return p.k == 128 && (p.n == 512 || p.n == 1024); }
+bool kw_applicable(const CodeParams &p) {
+  return p.k >= 16 && p.k <= 128 && (p.k & (p.k - 1)) == 0 && p.n > p.k && p.n <= 8 * p.k;
+}
 
-size_t k128w_scratch_bytes(const CodeParams &p) { return k128w_applicable(p) ? 256 : 0; }
+size_t kw_scratch_bytes(const CodeParams &p) { return kw_applicable(p) ? 256 : 0; }
 
-hipError_t launch_encode_k128w(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
-                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
-                               size_t sstride, void *scratch, hipStream_t s) {
+template <int M>
+static hipError_t launch_m(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads, size_t plen,
+                           size_t pstride, size_t batch, uint8_t *d_shards, size_t sstride, void *scratch,
+                           hipStream_t s) {
   int cus = 0;
-  if (!t.cimg) return hipErrorInvalidValue;
-  if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&encode_k128w), LDS_BYTES, &cus);
+  if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&encode_kw<M>), LDS_BYTES, &cus);
       e != hipSuccess)
     return e;
-  if (!k128w_applicable(p) || p.nv <= uint32_t(K) || p.nv > p.n) return hipErrorInvalidValue;
   const size_t sl = shard_len(p.k, plen);
-  const size_t tiles = (sl / 2 + TILE - 1) / TILE * batch;
+  const size_t tiles = (sl / 2 + Geo<M>::TILE - 1) / Geo<M>::TILE * batch;
   if (tiles >= (size_t(1) << 32) - size_t(4) * cus) return hipErrorInvalidValue;
   uint32_t *tick = static_cast<uint32_t *>(scratch);  // none: the static schedule
   if (tick)
     if (const hipError_t e = launch_zero_counters(tick, sizeof(uint32_t), s); e != hipSuccess) return e;
   const size_t slots = 2 * size_t(cus);  // two workgroups per CU
   const unsigned grid = unsigned(tiles < slots ? tiles : slots);
-  hipLaunchKernelGGL(encode_k128w, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads, uint64_t(plen),
+  hipLaunchKernelGGL(encode_kw<M>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads, uint64_t(plen),
                      uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride), int(p.nv),
                      uint32_t(batch), t.cimg, tick);
   return hipGetLastError();
+}
+
+hipError_t launch_encode_kw(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
+                            size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
+                            size_t sstride, void *scratch, hipStream_t s) {
+  if (!t.cimg || !kw_applicable(p) || p.nv <= p.k || p.nv > p.n) return hipErrorInvalidValue;
+  switch (p.k) {
+    case 16: return launch_m<4>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
+    case 32: return launch_m<5>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
+    case 64: return launch_m<6>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
+    default: return launch_m<7>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
+  }
 }
 
 }  // namespace ecamd

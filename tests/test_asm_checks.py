@@ -102,12 +102,15 @@ def test_enc_k512w_fast_store_count_no_spills(tmp_path):
     assert "scratch_" not in body
 
 
-def test_enc_k128w_fast_store_count_no_spills(tmp_path):
-    # enc_k128w.hip: store_own's fast path, 4 stores per lane (the compiler's
-    # own vmcnt(4) before the next tile's transposes counts them); no spills
-    text = _asm("enc_k128w.hip", tmp_path)
-    blocks = _nt_store_blocks(text, "encode_k128w")
-    assert blocks and all(c == 4 for c in blocks), blocks
-    body = text[text.index("encode_k128w"):]
-    body = body[:body.index("s_endpgm")]
-    assert "scratch_" not in body
+def test_enc_kw_fast_store_count_no_spills(tmp_path):
+    # enc_kw.hip (k = 16 .. 128): store_own's fast path, 4 stores per lane in
+    # every instantiation (the compiler's own vmcnt(4) before the next tile's
+    # transposes counts them); no spills
+    text = _asm("enc_kw.hip", tmp_path)
+    for m in (4, 5, 6, 7):
+        name = "encode_kwILi%dE" % m
+        blocks = _nt_store_blocks(text, name)
+        assert blocks and all(c == 4 for c in blocks), (m, blocks)
+        body = text[text.index(name + "EEvPKh"):]
+        body = body[:body.index("s_endpgm")]
+        assert "scratch_" not in body, m

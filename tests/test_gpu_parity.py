@@ -233,18 +233,23 @@ def test_encode_k512w_vs_oracle(oracle, nv, plen, batch, pad):
 
 
 @pytest.mark.parametrize("nv,plen,batch,pad", [
+    # k = 16 (n 64 / 128), 32 (128 / 256), 64 (256 / 512): first and last
+    # n_validators of the k, the n boundary
+    (46, 70001, 3, 64), (47, 1, 2, 16), (64, 32768, 2, 16), (65, 32769, 3, 8), (93, 100001, 2, 64),
+    (94, 33, 3, 16), (128, 3 * 32768, 2, 64), (129, 40001, 2, 8), (189, 65, 2, 64),
+    (190, 70001, 2, 16), (256, 129, 3, 64), (257, 32767, 2, 8), (300, 100001, 2, 64), (381, 32769, 2, 16),
+    # k = 128 (n 512 / 1024)
     (382, 70001, 3, 64), (383, 1, 2, 16), (384, 32768, 2, 16), (512, 32769, 3, 8),
     (513, 40001, 2, 64), (600, 255, 2, 16), (640, 3 * 32768, 2, 64), (641, 30001, 2, 8),
     (700, 257, 3, 64), (765, 100001, 3, 16), (765, 1_000_000, 2, 64)])
-def test_encode_k128w_vs_oracle(oracle, nv, plen, batch, pad):
-    """enc_k128w.hip (k = 128, n = 512 / 1024): the first and last
-    n_validators of each coset count (J = 2..5 cosets, the last partly below
-    n_validators), payloads of one piece, of whole and partial 128-piece tiles
-    (waves with no pieces), 8 / 16 / 64-byte row pitches, against the
-    reference encoder."""
+def test_encode_kw_vs_oracle(oracle, nv, plen, batch, pad):
+    """enc_kw.hip (k = 16 .. 128, n <= 8 k): the first and last n_validators
+    of each coset count (J = 2..5 cosets, the last partly below n_validators),
+    payloads of one piece, of whole and partial 32 KB tiles (waves with no
+    pieces), 8 / 16 / 64-byte row pitches, against the reference encoder."""
     import torch
     n, k, _ = E.code_params(nv)
-    assert k == 128
+    assert 16 <= k <= 128
     sl = E.shard_len(nv, plen)
     ss = (sl + pad - 1) // pad * pad
     pays = [synth.payload(nv * 5 + b, plen) for b in range(batch)]
@@ -1286,7 +1291,8 @@ def test_encode_ws_without_counter(oracle):
     caller that cached an older size would pass) runs the k = 256 / 512 / 1024
     encodes on their static tile schedule instead of failing; bit-exact."""
     import torch
-    for nv, plen, B in ((1024, 70_000, 5), (600, 50_000, 3), (2500, 60_000, 3), (4096, 80_000, 3)):
+    for nv, plen, B in ((1024, 70_000, 5), (600, 50_000, 3), (2500, 60_000, 3), (4096, 80_000, 3),
+                         (300, 40_000, 2), (100, 40_000, 2)):
         n, k, thr = E.code_params(nv)
         assert E.workspace_bytes(nv, plen, B)[0] == 256, nv
         sl = E.shard_len(nv, plen)
