@@ -2,7 +2,7 @@
 // 1024), any k with 16 <= k < n: the n_validators the n = 1024 / k = 256
 // kernel does not cover (e.g. 512..765 validators: n = 1024, k = 128).
 //
-// As in enc_gen.hip, a wave's 1024 positions (tf1024.hpp: 64 lanes x 16
+// A wave's 1024 positions (tf1024.hpp: 64 lanes x 16
 // registers, 4 codewords per byte-planar register) are read as 1024 / n
 // independent n-point codewords: position = (instance << L) | local.  Per
 // codeword (decode_main, poly_encoder.hpp:164-189):

@@ -558,10 +558,10 @@ hipError_t launch_signal_host(uint32_t *h_flag, uint32_t v, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Encode scratch that is only a tile counter (k = 256 / 512 / 1024 fast
+// Encode scratch that is only a tile counter (the k = 16 .. 1024 fast
 // kernels): optional, the kernels fall back to a static schedule without it.
 bool encode_scratch_optional(const CodeParams &p) {
-  return k1024_applicable(p) || k256_applicable(p) || k512w_applicable(p) || kw_applicable(p) || encgen_applicable(p);
+  return k1024_applicable(p) || k256_applicable(p) || k512w_applicable(p) || kw_applicable(p);
 }
 
 size_t encode_scratch_bytes(const CodeParams &p, size_t plen, size_t batch) {
@@ -569,7 +569,6 @@ size_t encode_scratch_bytes(const CodeParams &p, size_t plen, size_t batch) {
   if (k256_applicable(p)) return k256_scratch_bytes(p);
   if (k512w_applicable(p)) return k512w_scratch_bytes(p);
   if (kw_applicable(p)) return kw_scratch_bytes(p);
-  if (encgen_applicable(p)) return encgen_scratch_bytes(p);
   if (p.k <= uint32_t(kLdsSlots)) return 0;
   const size_t pieces = shard_len(p.k, plen) / 2;
   const size_t tiles = (pieces + 3) / 4;
@@ -593,8 +592,6 @@ hipError_t launch_encode(const CodeParams &p, const DevTables &t, const uint8_t 
     return launch_encode_k512w(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
   if (aligned && kw_applicable(p))
     return launch_encode_kw(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
-  if (aligned && encgen_applicable(p))
-    return launch_encode_gen(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
   if (aligned && k1024_applicable(p))
     return launch_encode_k1024(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
   const size_t sl = shard_len(p.k, plen);

@@ -209,14 +209,6 @@ hipError_t launch_encode_kw(const CodeParams &p, const DevTables &t, const uint8
                             size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                             size_t sstride, void *scratch, hipStream_t s);
 
-// register-blocked encode for k = 16 .. 512, n <= 4096 (enc_gen.hip)
-bool encgen_applicable(const CodeParams &p);
-// scratch (nullable: static tile schedule): encgen_scratch_bytes, the tile counter
-size_t encgen_scratch_bytes(const CodeParams &p);
-hipError_t launch_encode_gen(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
-                             size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
-                             size_t sstride, void *scratch, hipStream_t s);
-
 // Per-payload gather order of the received rows, present rows first, per
 // 1024-row quarter (or the n < 1024 rows; dec_n1024.hip): the scratch of
 // reconstruct_n1024, _n4096 and _gen, gather_order_bytes(p, batch)

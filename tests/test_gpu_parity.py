@@ -180,7 +180,7 @@ def _batch_case(nv, plen, batch, cnt_key="threshold", seed0=0, pad=0):
     # k = 1024 / n = 4096 fast path (config 4): several 64-piece tiles, a partly
     # populated last coset (nv 3500), tight and 8/16/64-byte row pitches
     (4096, 300001, 2, 64), (3070, 300001, 2, 16), (3500, 131073, 2, 8), (4096, 131072, 1, 0),
-    # k = 32 / 64 / 128, n <= 1024 register-blocked encode: several tiles,
+    # k = 32 / 64 / 128, n <= 1024 encode (encode_kw): several tiles,
     # partly populated last cosets, 8/16/64-byte pitches
     (600, 300001, 2, 64), (700, 5000, 2, 64), (384, 131073, 2, 64), (300, 70001, 3, 16),
     (100, 12345, 3, 8), (200, 200001, 2, 64),
@@ -188,8 +188,9 @@ def _batch_case(nv, plen, batch, cnt_key="threshold", seed0=0, pad=0):
     # shape): several tiles, partial last tile, 16/64-byte pitches
     (46, 70001, 2, 64), (65, 9999, 3, 16), (129, 33333, 2, 16), (257, 100001, 2, 64),
     (512, 200001, 2, 64), (765, 300001, 2, 64), (600, 1, 2, 16),
-    # n = 2048 / 4096 with k = 256 / 512: encode with per-coset table images,
-    # reconstruct by halves / quarters with k < 1024 outputs
+    # n = 2048 / 4096 with k = 256 / 512: encode with per-coset table images
+    # (encode_k256<2048>, encode_k512w), reconstruct by halves / quarters
+    # with k < 1024 outputs
     (1025, 5000, 3, 64), (1500, 200001, 2, 64), (2048, 100001, 2, 16), (2500, 300001, 2, 64),
     (3069, 4097, 2, 16)])
 def test_batch_vs_oracle(oracle, nv, plen, batch, pad):
