@@ -84,6 +84,7 @@ def main():
         for v in order:
             evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(a.steps)]
             d_out.zero_()
+            d_sh.zero_()  # a variant that does not write its shards fails the round trip
             for ev in evs:
                 step(libs[v], ev)
             torch.cuda.synchronize()
