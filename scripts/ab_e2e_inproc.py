@@ -64,11 +64,13 @@ def main():
     for L in libs.values():  # warm: every variant's pipeline slots
         enc(L)
         rec(L)
+    ref_sh = c["sh"].clone()  # the shards every variant must write (zeroed before each encode)
     gib = c["B"] * a.payload / 2**30
     for r in range(a.rounds):
         order = a.variants[r % len(a.variants):] + a.variants[:r % len(a.variants)]
         for v in order:
             L = libs[v]
+            c["sh"].zero_()
             t0 = time.perf_counter()
             enc(L)
             t1 = time.perf_counter()
@@ -79,6 +81,7 @@ def main():
             res[v]["enc"].append(gib / (t1 - t0))
             res[v]["rec"].append(gib / (t3 - t2))
             res[v]["ok"] &= bool(torch.equal(c["out"][:, :a.payload], c["pay"]))
+            res[v]["ok"] &= bool(torch.equal(c["sh"], ref_sh))
     for v in a.variants:
         d = res[v]
         print(f"{v:10s} encode {statistics.median(d['enc']):.3f} reconstruct {statistics.median(d['rec']):.3f} "
