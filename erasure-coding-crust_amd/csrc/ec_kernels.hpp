@@ -63,6 +63,10 @@ __host__ __device__ constexpr uint32_t cimg_lin(uint32_t x) {
 constexpr uint32_t kEImg512Bytes = 35840, kEImg512Cosets = 7;
 constexpr uint32_t kEImg512Stage[3] = {0, 20480, 30720};
 
+// The same for the k = 256, n = 2048 encode (enc_kw.hip): stage 0 of cosets
+// j = 4..7 (elements 128 j + e, e < 128), plane q at q * 2048 + cimg_lin(e).
+constexpr uint32_t kEImg256Bytes = 10240, kEImg256Cosets = 4;
+
 // Reduced F9 image 0 (reconstruct_n1024x, 12 waves per CU): planes 0 and 1 of
 // every slot as in the F9 image (kind 0) at 0 / 16384 (the subfield tables of
 // stages >= 2 use only those), planes 2, 3 of the stage-0 (general) and
@@ -83,6 +87,7 @@ struct DevTables {
   const MulTab *mslot = nullptr;       // 65535, mslot[i] = mtab[skews[i]]: by skew slot, one load
   const uint8_t *dimg = nullptr;       // kDImgBytes, the reduced F9 image 0
   const uint8_t *eimg512 = nullptr;    // kEImg512Cosets x kEImg512Bytes, the k = 512 encode's coset images
+  const uint8_t *eimg256 = nullptr;    // kEImg256Cosets x kEImg256Bytes, the k = 256 / n = 2048 encode's
 };
 
 // Completion signal of a per-call C-ABI call fused into its last kernel: when
@@ -201,8 +206,9 @@ hipError_t launch_encode_k512w(const CodeParams &p, const DevTables &t, const ui
                                size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                                size_t sstride, void *scratch, hipStream_t s);
 
-// k = 16 .. 128, n <= 8 k (enc_kw.hip): the same model on the compact image
-// alone; scratch (nullable) the tile counter, kw_scratch_bytes
+// k = 16 .. 128, n <= 8 k, and k = 256 at n = 2048 (enc_kw.hip): the same
+// model on the compact image (+ coset extension tables at k = 256); scratch
+// (nullable) the tile counter, kw_scratch_bytes
 bool kw_applicable(const CodeParams &p);
 size_t kw_scratch_bytes(const CodeParams &p);
 hipError_t launch_encode_kw(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,

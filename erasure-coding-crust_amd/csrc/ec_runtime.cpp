@@ -25,6 +25,7 @@ struct DeviceState {
   uint8_t *cimg = nullptr;
   uint8_t *dimg = nullptr;
   uint8_t *eimg512 = nullptr;
+  uint8_t *eimg256 = nullptr;
   MulTab *mslot = nullptr;  // mtab by skew slot (DevTables::mslot)
   std::mutex mu;
   std::map<uint32_t, uint16_t *> fold;
@@ -169,6 +170,17 @@ DeviceState *device_state() {
           std::memcpy(&eimg[(j - 1) * kEImg512Bytes + kEImg512Stage[m] + q * (4096 >> m) + cimg_lin(e)],
                       &g.w[4 * q], 16);
       }
+  std::vector<uint8_t> eimg256(kEImg256Cosets * kEImg256Bytes, 0);
+  for (uint32_t j = 4; j < 4 + kEImg256Cosets; ++j)
+    for (uint32_t e = 0; e < 128; ++e) {
+      const MulTab g = f.tower_tab(f.log[2 * (128 * j + e)]);
+      for (uint32_t q = 0; q < 5; ++q)
+        std::memcpy(&eimg256[(j - 4) * kEImg256Bytes + q * 2048 + cimg_lin(e)], &g.w[4 * q], 16);
+    }
+  if (!hip_ok(hipMalloc(&st->eimg256, eimg256.size()), "hipMalloc(k256 coset images)") ||
+      !hip_ok(hipMemcpy(st->eimg256, eimg256.data(), eimg256.size(), hipMemcpyHostToDevice),
+              "upload k256 coset images"))
+    return nullptr;
   if (!hip_ok(hipMalloc(&st->eimg512, eimg.size()), "hipMalloc(k512 coset images)") ||
       !hip_ok(hipMemcpy(st->eimg512, eimg.data(), eimg.size(), hipMemcpyHostToDevice),
               "upload k512 coset images"))
@@ -238,6 +250,7 @@ DevTables device_tables(DeviceState *d) {
   t.mslot = d->mslot;
   t.dimg = d->dimg;
   t.eimg512 = d->eimg512;
+  t.eimg256 = d->eimg256;
   return t;
 }
 

@@ -650,7 +650,7 @@ bool k256_packed_ok(size_t plen, size_t batch, uintptr_t sh, size_t sstride) {
   return sh % 2 == 0 && sstride % 2 == 0 && npp8 * batch + TILE < (size_t(1) << 32);
 }  // (npp8 >= npp: also bounds the exactly flattened piece space of PK = 2)
 
-size_t k256_scratch_bytes(const CodeParams &p) { return p.n == 1024 ? 256 : 0; }
+size_t k256_scratch_bytes(const CodeParams &) { return 256; }  // the unpacked kernels' tile counter
 
 hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uint8_t *d_payloads,
                               size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
@@ -660,6 +660,8 @@ hipError_t launch_encode_k256(const CodeParams &p, const DevTables &t, const uin
                                   reinterpret_cast<uintptr_t>(d_shards), sstride);
   if (p.n == 1024 && !packed)
     return launch_encode_k256w(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
+  if (p.n == 2048 && !packed)  // round 6: the two-workgroups-per-CU model (enc_kw.hip)
+    return launch_encode_kw(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
   if (packed && !k256_packed_ok(plen, batch, reinterpret_cast<uintptr_t>(d_shards), sstride))
     return hipErrorInvalidValue;
   const void *fn = p.n == 1024 ? reinterpret_cast<const void *>(&encode_k256<1024, 2>)

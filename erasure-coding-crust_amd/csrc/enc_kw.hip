@@ -26,6 +26,8 @@
 #include "cimg.hpp"
 #include "enc_k256_common.hpp"
 
+#include <type_traits>
+
 namespace ecamd {
 namespace {
 
@@ -34,8 +36,12 @@ constexpr int THREADS = 64 * WAVES;
 constexpr uint32_t XCH0 = kCImgBytes;        // the wave regions follow the tables
 constexpr uint32_t XCH_BYTES = 4096;
 constexpr uint32_t SLOT = XCH0 + WAVES * XCH_BYTES;  // the next tile's index
-constexpr int LDS_BYTES = int(SLOT + 16);
-static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
+// k = 256 (n = 2048 only): the extension tables of cosets 4..7 (stage 0,
+// elements 512..1023: ec_kernels.hpp kEImg256*) after the slot
+constexpr uint32_t EXT8 = SLOT + 1024;
+template <int M>
+constexpr int lds_bytes() { return int(M == 8 ? EXT8 + kEImg256Bytes : SLOT + 16); }
+static_assert(2 * lds_bytes<8>() <= 160 * 1024, "two workgroups per CU");
 static_assert(XCH0 % (2 * XCH_BYTES) == 0, "XOR-addressed regions");
 static_assert(kCImgBytes % (16 * THREADS) == 0, "whole image chunks per thread");
 
@@ -48,7 +54,7 @@ struct Geo {
   static constexpr int RC = 4 * NG;            // 16-B chunks per shard-row segment
   static constexpr int RPI = 512 / RC;         // rows per store iteration (all waves), 0 if < 1
   static constexpr uint32_t QM = (1u << (M - 3)) - 1;  // lane mask of the layout-A position part
-  static_assert(M >= 4 && M <= 7, "k = 16 .. 128");
+  static_assert(M >= 4 && M <= 8, "k = 16 .. 256");
 };
 
 struct XLanes {
@@ -83,32 +89,97 @@ __device__ __forceinline__ void ipass(State &s, uint32_t base) {
   for (int r = 0; r < 4; ++r) ibfly(s, r, r + 4, Ta2);
 }
 
+// Table kinds of a stage: the compact image's subfield / F9 / general entries
+// (SubTab, F9Tab, Tab), or (k = 256 at n = 2048, stage 0 of cosets 4..7) a
+// general table of the coset's extension image in LDS (Ext0)
+struct Ext0 {};
+template <typename K_>
+struct TabOf {
+  using type = K_;
+};
+template <>
+struct TabOf<Ext0> {
+  using type = Tab;
+};
+// table of element x = lane part lt ^ block part r ^ uniform part u (each the
+// cimg_lin of its bits); an extension table sits at the coset-local entry
+// (u, the coset's offset bits, dropped)
+template <typename K_>
+__device__ __forceinline__ void ftab(uint32_t lt, uint32_t r, uint32_t u, typename TabOf<K_>::type &T) {
+  if constexpr (std::is_same_v<K_, Ext0>) {
+    const uint32_t a = lt ^ r;
+#pragma unroll
+    for (int q = 4; q >= 0; --q) {
+      const v4u v = lds_r128(a + EXT8 + uint32_t(q) * (kEImg256Bytes / 5));
+      T.t[4 * q] = v.x;
+      T.t[4 * q + 1] = v.y;
+      T.t[4 * q + 2] = v.z;
+      T.t[4 * q + 3] = v.w;
+    }
+  } else {
+    ctab(lt, r ^ u, T);
+  }
+}
+
 // forward radix-8 pass at index off: stages B0+2, B0+1, B0 with table kinds
-// T2, T1, T0 (known per coset)
-template <int B0, typename T2, typename T1, typename T0>
+// K2, K1, K0 (known per coset)
+template <int B0, typename K2, typename K1, typename K0>
 __device__ __forceinline__ void fpass(State &s, uint32_t base, uint32_t off) {
   const XLanes x = xlanes<B0>(base);
   const uint32_t u0 = cimg_lin(off >> (B0 + 1)), u1 = cimg_lin(off >> (B0 + 2)), u2 = cimg_lin(off >> (B0 + 3));
-  T2 Ta2;
-  T1 Ta1, Tb1;
-  T0 Ta0, Tb0;
-  ctab(x.l2, u2, Ta2);
-  ctab(x.l1, u1, Tb1);
+  typename TabOf<K2>::type Ta2;
+  typename TabOf<K1>::type Ta1, Tb1;
+  typename TabOf<K0>::type Ta0, Tb0;
+  ftab<K2>(x.l2, 0u, u2, Ta2);
+  ftab<K1>(x.l1, 0u, u1, Tb1);
 #pragma unroll
   for (int r = 0; r < 4; ++r) fbfly(s, r, r + 4, Ta2);
-  ctab(x.l1, u1 ^ cimg_lin(1), Ta1);
+  ftab<K1>(x.l1, cimg_lin(1), u1, Ta1);
   fbfly(s, 0, 2, Tb1);
   fbfly(s, 1, 3, Tb1);
-  ctab(x.l0, u0, Tb0);
+  ftab<K0>(x.l0, 0u, u0, Tb0);
   fbfly(s, 4, 6, Ta1);
   fbfly(s, 5, 7, Ta1);
-  ctab(x.l0, u0 ^ cimg_lin(1), Ta0);
+  ftab<K0>(x.l0, cimg_lin(1), u0, Ta0);
   fbfly(s, 0, 1, Tb0);
-  ctab(x.l0, u0 ^ cimg_lin(2), Tb0);
+  ftab<K0>(x.l0, cimg_lin(2), u0, Tb0);
   fbfly(s, 2, 3, Ta0);
-  ctab(x.l0, u0 ^ cimg_lin(3), Ta0);
+  ftab<K0>(x.l0, cimg_lin(3), u0, Ta0);
   fbfly(s, 4, 5, Tb0);
   fbfly(s, 6, 7, Ta0);
+}
+
+// ---- layout C for k = 256 (register bit 0 = p6, bit 1 = p7, bit 2 = p5):
+// the elements of stages 6, 7 are lane-uniform (enc_k256w.hip ipassC0w /
+// fpassCw).  IFFT at index 0: stage 7 (x = 0) and stage 6's p7 = 0 block (x =
+// 0) are b ^= a only; stage 6's p7 = 1 block has x = 1.
+__device__ __forceinline__ void ipassC8(State &s) {
+  SubTab Tb;
+  ctab(0u, cimg_lin(1), Tb);
+  bxor(s, 0, 1);
+  bxor(s, 4, 5);
+  ibfly(s, 2, 3, Tb);
+  ibfly(s, 6, 7, Tb);
+  bxor(s, 0, 2);
+  bxor(s, 1, 3);
+  bxor(s, 4, 6);
+  bxor(s, 5, 7);
+}
+// FFT stages 7, 6 at index off from the IFFT coefficients c: stage 7 x = off
+// >> 8, stage 6 x = off >> 7 | p7
+__device__ __forceinline__ void fpassC8(State &s, const State &c, uint32_t off) {
+  SubTab Ta, Tb;
+  ctab(0u, cimg_lin(off >> 8), Ta);
+  ctab(0u, cimg_lin(off >> 7), Tb);
+  fbfly_from(s, c, 0, 2, Ta);
+  fbfly_from(s, c, 1, 3, Ta);
+  fbfly_from(s, c, 4, 6, Ta);
+  fbfly_from(s, c, 5, 7, Ta);
+  ctab(0u, cimg_lin((off >> 7) | 1u), Ta);
+  fbfly(s, 0, 1, Tb);
+  fbfly(s, 4, 5, Tb);
+  fbfly(s, 2, 3, Ta);
+  fbfly(s, 6, 7, Ta);
 }
 
 // ---- layout B for M <= 6: registers p3, p4, p5 as far as they are positions
@@ -208,9 +279,16 @@ __device__ __forceinline__ void xchg(State &s, XBase xb) {
 // M) ^ ((w << (9 - M)) & 31).  Layout-A writes (rows 8 q + r; 32 lanes = the
 // q and the low group bits) and the store reads (16 lanes x 16 B = group pairs
 // (2h, 2h + 1) of one row across waves) hit distinct banks.
+// k = 256 (NG = 2): bit 0 stays the group (a store read takes groups 0 and 1
+// of a row as one 16-B pair), the row's bits 3-6 go to bits 1-4 (16-lane
+// write groups distinct) and the wave to bits 2-4 (the two rows of a 16-lane
+// store read, which differ in bit 1, keep their 8 chunks apart).
 template <int M>
 __host__ __device__ constexpr uint32_t soff(uint32_t v, uint32_t g, uint32_t w) {
-  return (((v << (9 - M)) | g) ^ ((v >> 3) << (8 - M)) ^ ((w << (9 - M)) & 31u)) << 3;
+  if constexpr (M == 8)
+    return (((v << 1) | g) ^ (((v >> 3) & 15u) << 1) ^ ((w << 2) & 31u)) << 3;
+  else
+    return (((v << (9 - M)) | g) ^ ((v >> 3) << (8 - M)) ^ ((w << (9 - M)) & 31u)) << 3;
 }
 
 template <int M>
@@ -304,6 +382,7 @@ __global__ void __launch_bounds__(THREADS, 4) encode_kw(const uint8_t *__restric
                                                         uint8_t *__restrict__ shards, uint64_t slen,
                                                         uint64_t sstride, int nv, uint32_t batch,
                                                         const uint8_t *__restrict__ cimg,
+                                                        const uint8_t *__restrict__ eimg,
                                                         uint32_t *__restrict__ tick) {
   using G = Geo<M>;
   constexpr uint32_t K = G::K;
@@ -387,6 +466,18 @@ __global__ void __launch_bounds__(THREADS, 4) encode_kw(const uint8_t *__restric
     if (tid0 == 0) taken = tick ? atomicAdd(tick, 1u) : cur + gridDim.x;
     uint32_t next = 0;
     uint8_t *SH = shards + b * uint64_t(nv) * sstride;
+    // every store phase of this tile but possibly the last coset's takes the
+    // fast path (4 stores per lane), or none does
+    const bool fast = store_fast<M>(SH, sstride, 0, nv, piece0, npieces);
+    (void)fast;
+    // k = 256, n = 2048: coset j's extension image (10 x 1 KB) -> LDS, chunk i by
+    // wave i % 8, issued after the previous coset's rows-staged barrier
+    const auto dma_ext = [&](uint32_t j) __attribute__((always_inline)) {
+      const uint8_t *src = eimg + (j - 4) * kEImg256Bytes + 16 * lane;
+      for (uint32_t i = wave_s; i < kEImg256Bytes / 1024; i += WAVES)
+        lds_dma16(EXT8 + 1024 * i, src + 1024 * i);
+    };
+    (void)dma_ext;
     const auto fetch_next = [&]() __attribute__((always_inline)) {
       next = __builtin_amdgcn_readfirstlane(*slot);
       fetch(next < total ? next / tiles_pp : 0, next < total ? next % tiles_pp : tiles_pp);
@@ -417,6 +508,10 @@ __global__ void __launch_bounds__(THREADS, 4) encode_kw(const uint8_t *__restric
       store_sys();
       rsync();  // after IFFT pass A
       for (uint32_t j = 1;; ++j) {
+        if constexpr (M == 8) {
+          if (j >= 4 && fast) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+          else if (j >= 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         rsync();  // previous rows read out
         if (j == J) {
           fetch_next();
@@ -425,6 +520,8 @@ __global__ void __launch_bounds__(THREADS, 4) encode_kw(const uint8_t *__restric
           break;
         }
         rsync();  // rows staged
+        if constexpr (M == 8)
+          if (j >= 3) dma_ext(j + 1);
         store(K * j, false);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -449,11 +546,15 @@ __global__ void __launch_bounds__(THREADS, 4) encode_kw(const uint8_t *__restric
     // ---- IFFT_k (index 0): pass A (bits 0-2), then pass B (bits 3..M-1;
     // M = 7: 3-5, then stage 6 in layout C).  Lane parts of the positions
     // (group bits excluded): A 8 q, B (M = 7) posB(q5, 0) & 127
-    const uint32_t baseA = 8 * q, baseB = posB(q5, 0) & 127u;
+    const uint32_t baseA = 8 * q, baseB = posB(q5, 0) & (K - 1);
     ipass<0>(s, baseA);
     rsync();  // systematic rows read out of the regions
     xchg<LA, LB>(s, xb);
-    if constexpr (M == 7) {
+    if constexpr (M == 8) {
+      ipass<3>(s, baseB);
+      xchg<LB, LC>(s, xb);
+      ipassC8(s);
+    } else if constexpr (M == 7) {
       ipass<3>(s, baseB);
       xchg<LB, LC>(s, xb);
 #pragma unroll
@@ -467,7 +568,8 @@ __global__ void __launch_bounds__(THREADS, 4) encode_kw(const uint8_t *__restric
     // Kinds (x = (pos + off) >> (m + 1)): M = 7: stage 0 subfield (j = 1), F9
     // (2, 3), general (4..7), stage 1 subfield (j <= 3), F9 above; M = 6:
     // stage 0 subfield (j <= 3), F9 above; everything else subfield.
-    const auto coset = [&](auto t1, auto t0, const uint32_t j) __attribute__((always_inline)) {
+    const auto coset = [&](auto t2, auto t1, auto t0, const uint32_t j) __attribute__((always_inline)) {
+      using T2 = decltype(t2);
       using T1 = decltype(t1);
       using T0 = decltype(t0);
       const uint32_t off = K * j;
@@ -475,7 +577,17 @@ __global__ void __launch_bounds__(THREADS, 4) encode_kw(const uint8_t *__restric
       asm volatile("" : "+v"(bA), "+v"(bB));  // table addresses formed per coset, not hoisted
 #pragma unroll
       for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(coef.l[0][r]), "+v"(coef.h[0][r]));
-      if constexpr (M == 7) {
+      if constexpr (M == 8) {
+        fpassC8(s, coef, off);
+        // previous coset's rows read out; from coset 4 on, also this coset's
+        // extension image landed in every wave (issued before the previous
+        // coset's store phase: 4 stores per lane after it on the fast path)
+        if (j >= 4 && fast) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (j >= 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        rsync();
+        xchg<LC, LB>(s, xb);
+        fpass<3, SubTab, SubTab, SubTab>(s, bB, off);
+      } else if constexpr (M == 7) {
         {  // stage 6, x = off >> 7, from the coefficients
           SubTab T6;
           ctab(0u, cimg_lin(off >> 7), T6);
@@ -490,7 +602,7 @@ __global__ void __launch_bounds__(THREADS, 4) encode_kw(const uint8_t *__restric
         rsync();  // previous coset's rows read out
       }
       xchg<LB, LA>(s, xb);
-      fpass<0, SubTab, T1, T0>(s, bA, off);
+      fpass<0, T2, T1, T0>(s, bA, off);
       {  // back to symbol coordinates
         const TowerK tk = tower_k();
 #pragma unroll
@@ -501,15 +613,19 @@ __global__ void __launch_bounds__(THREADS, 4) encode_kw(const uint8_t *__restric
     // the cosets in a loop (a body per table-kind class); the last one leaves
     // it, so the next tile's payload (d, nxt) is live in that one only
     for (uint32_t j = 1;; ++j) {
-      if constexpr (M == 7) {
-        if (j == 1) coset(SubTab(), SubTab(), j);
-        else if (j <= 3) coset(SubTab(), F9Tab(), j);
-        else coset(F9Tab(), Tab(), j);
+      if constexpr (M == 8) {  // n = 2048: stage 0 of cosets 4..7 from the extension image
+        if (j == 1) coset(SubTab(), SubTab(), F9Tab(), j);
+        else if (j <= 3) coset(SubTab(), F9Tab(), Tab(), j);
+        else coset(F9Tab(), Tab(), Ext0(), j);
+      } else if constexpr (M == 7) {
+        if (j == 1) coset(SubTab(), SubTab(), SubTab(), j);
+        else if (j <= 3) coset(SubTab(), SubTab(), F9Tab(), j);
+        else coset(SubTab(), F9Tab(), Tab(), j);
       } else if constexpr (M == 6) {
-        if (j <= 3) coset(SubTab(), SubTab(), j);
-        else coset(SubTab(), F9Tab(), j);
+        if (j <= 3) coset(SubTab(), SubTab(), SubTab(), j);
+        else coset(SubTab(), SubTab(), F9Tab(), j);
       } else {
-        coset(SubTab(), SubTab(), j);
+        coset(SubTab(), SubTab(), SubTab(), j);
       }
       if (j == J) {
         fetch_next();  // coef and s are dead here
@@ -517,16 +633,20 @@ __global__ void __launch_bounds__(THREADS, 4) encode_kw(const uint8_t *__restric
         store(K * j, true);
         break;
       }
-      rsync();  // rows staged
+      rsync();  // rows staged; every wave is past this coset's tables
+      if constexpr (M == 8)
+        if (j >= 3) dma_ext(j + 1);
       store(K * j, false);
       __builtin_amdgcn_sched_barrier(0);
     }
     cur = next;
   }
+  if constexpr (M == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
 }
 
 bool kw_applicable(const CodeParams &p) {
-  return p.k >= 16 && p.k <= 128 && (p.k & (p.k - 1)) == 0 && p.n > p.k && p.n <= 8 * p.k;
+  return (p.k >= 16 && p.k <= 128 && (p.k & (p.k - 1)) == 0 && p.n > p.k && p.n <= 8 * p.k) ||
+         (p.k == 256 && p.n == 2048);
 }
 
 size_t kw_scratch_bytes(const CodeParams &p) { return kw_applicable(p) ? 256 : 0; }
@@ -536,7 +656,7 @@ static hipError_t launch_m(const CodeParams &p, const DevTables &t, const uint8_
                            size_t pstride, size_t batch, uint8_t *d_shards, size_t sstride, void *scratch,
                            hipStream_t s) {
   int cus = 0;
-  if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&encode_kw<M>), LDS_BYTES, &cus);
+  if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&encode_kw<M>), lds_bytes<M>(), &cus);
       e != hipSuccess)
     return e;
   const size_t sl = shard_len(p.k, plen);
@@ -547,9 +667,9 @@ static hipError_t launch_m(const CodeParams &p, const DevTables &t, const uint8_
     if (const hipError_t e = launch_zero_counters(tick, sizeof(uint32_t), s); e != hipSuccess) return e;
   const size_t slots = 2 * size_t(cus);  // two workgroups per CU
   const unsigned grid = unsigned(tiles < slots ? tiles : slots);
-  hipLaunchKernelGGL(encode_kw<M>, dim3(grid), dim3(THREADS), LDS_BYTES, s, d_payloads, uint64_t(plen),
+  hipLaunchKernelGGL(encode_kw<M>, dim3(grid), dim3(THREADS), lds_bytes<M>(), s, d_payloads, uint64_t(plen),
                      uint64_t(pstride), d_shards, uint64_t(sl), uint64_t(sstride), int(p.nv),
-                     uint32_t(batch), t.cimg, tick);
+                     uint32_t(batch), t.cimg, t.eimg256, tick);
   return hipGetLastError();
 }
 
@@ -557,11 +677,13 @@ hipError_t launch_encode_kw(const CodeParams &p, const DevTables &t, const uint8
                             size_t plen, size_t pstride, size_t batch, uint8_t *d_shards,
                             size_t sstride, void *scratch, hipStream_t s) {
   if (!t.cimg || !kw_applicable(p) || p.nv <= p.k || p.nv > p.n) return hipErrorInvalidValue;
+  if (p.k == 256 && (!t.eimg256 || p.nv <= 4 * p.k)) return hipErrorInvalidValue;  // cosets 4.. exist (n = 2048)
   switch (p.k) {
     case 16: return launch_m<4>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
     case 32: return launch_m<5>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
     case 64: return launch_m<6>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
-    default: return launch_m<7>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
+    case 128: return launch_m<7>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
+    default: return launch_m<8>(p, t, d_payloads, plen, pstride, batch, d_shards, sstride, scratch, s);
   }
 }
 

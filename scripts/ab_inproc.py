@@ -15,6 +15,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "erasure-coding-crust_amd"))
@@ -46,6 +47,8 @@ def main():
     ap.add_argument("--nv", type=int, default=1024)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--gap-ms", type=float, default=0.0,
+                    help="synchronise and idle this long between the locator and the reconstruct")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     libs = {v: load(v) for v in a.variants}
@@ -70,6 +73,9 @@ def main():
         assert L.ECCR_AMD_encode_batch(nv, P(d_pay), plen, plen, B, P(d_sh), ss, sp).tag == 0
         ev[1].record(st)
         assert L.ECCR_AMD_error_locator(nv, P(d_pres), B, P(d_el), sp).tag == 0
+        if a.gap_ms > 0:
+            torch.cuda.synchronize()
+            time.sleep(a.gap_ms / 1000)
         ev[2].record(st)
         assert L.ECCR_AMD_reconstruct_batch(nv, P(d_sh), sl, ss, P(d_pres), P(d_el), B, P(d_out),
                                             sl * k, sp).tag == 0

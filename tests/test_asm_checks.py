@@ -103,11 +103,12 @@ def test_enc_k512w_fast_store_count_no_spills(tmp_path):
 
 
 def test_enc_kw_fast_store_count_no_spills(tmp_path):
-    # enc_kw.hip (k = 16 .. 128): store_own's fast path, 4 stores per lane in
+    # enc_kw.hip (k = 16 .. 256): store_own's fast path, 4 stores per lane in
     # every instantiation (the compiler's own vmcnt(4) before the next tile's
-    # transposes counts them); no spills
+    # transposes counts them, and at k = 256 the hand-written vmcnt(4) before
+    # a coset's extension tables); no spills
     text = _asm("enc_kw.hip", tmp_path)
-    for m in (4, 5, 6, 7):
+    for m in (4, 5, 6, 7, 8):
         name = "encode_kwILi%dE" % m
         blocks = _nt_store_blocks(text, name)
         assert blocks and all(c == 4 for c in blocks), (m, blocks)

@@ -222,9 +222,12 @@ def test_encode_k512w_vs_oracle(oracle, nv, plen, batch, pad):
     sl = E.shard_len(nv, plen)
     ss = (sl + pad - 1) // pad * pad
     pays = [synth.payload(nv * 3 + b, plen) for b in range(batch)]
-    d_pay = torch.from_numpy(np.stack(pays)).cuda()
+    ps = (plen + 63) // 64 * 64  # 16-B aligned payload rows: the fast kernels take ragged lengths too
+    d_pay = torch.zeros((batch, ps), dtype=torch.uint8, device="cuda")
+    for b in range(batch):
+        d_pay[b, :plen] = torch.from_numpy(pays[b])
     d_sh = torch.full((batch, nv, ss), 0x5C, dtype=torch.uint8, device="cuda")
-    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+    E.encode_batch(nv, d_pay, plen, ps, batch, d_sh, ss)
     torch.cuda.synchronize()
     got = d_sh.cpu().numpy()
     for b in range(batch):
@@ -239,24 +242,31 @@ def test_encode_k512w_vs_oracle(oracle, nv, plen, batch, pad):
     (46, 70001, 3, 64), (47, 1, 2, 16), (64, 32768, 2, 16), (65, 32769, 3, 8), (93, 100001, 2, 64),
     (94, 33, 3, 16), (128, 3 * 32768, 2, 64), (129, 40001, 2, 8), (189, 65, 2, 64),
     (190, 70001, 2, 16), (256, 129, 3, 64), (257, 32767, 2, 8), (300, 100001, 2, 64), (381, 32769, 2, 16),
+    # k = 256 at n = 2048 (4 and 5 cosets, stage 0 of cosets 4.. from the
+    # extension image)
+    (1025, 70001, 3, 64), (1100, 1, 2, 16), (1280, 32768, 2, 16), (1281, 32769, 3, 8),
+    (1400, 255, 2, 64), (1533, 100001, 3, 16), (1533, 1_000_000, 2, 64),
     # k = 128 (n 512 / 1024)
     (382, 70001, 3, 64), (383, 1, 2, 16), (384, 32768, 2, 16), (512, 32769, 3, 8),
     (513, 40001, 2, 64), (600, 255, 2, 16), (640, 3 * 32768, 2, 64), (641, 30001, 2, 8),
     (700, 257, 3, 64), (765, 100001, 3, 16), (765, 1_000_000, 2, 64)])
 def test_encode_kw_vs_oracle(oracle, nv, plen, batch, pad):
-    """enc_kw.hip (k = 16 .. 128, n <= 8 k): the first and last n_validators
+    """enc_kw.hip (k = 16 .. 128, n <= 8 k; k = 256, n = 2048): the first and last n_validators
     of each coset count (J = 2..5 cosets, the last partly below n_validators),
     payloads of one piece, of whole and partial 32 KB tiles (waves with no
     pieces), 8 / 16 / 64-byte row pitches, against the reference encoder."""
     import torch
     n, k, _ = E.code_params(nv)
-    assert 16 <= k <= 128
+    assert 16 <= k <= 128 or (k, n) == (256, 2048)
     sl = E.shard_len(nv, plen)
     ss = (sl + pad - 1) // pad * pad
     pays = [synth.payload(nv * 5 + b, plen) for b in range(batch)]
-    d_pay = torch.from_numpy(np.stack(pays)).cuda()
+    ps = (plen + 63) // 64 * 64  # 16-B aligned payload rows: the fast kernels take ragged lengths too
+    d_pay = torch.zeros((batch, ps), dtype=torch.uint8, device="cuda")
+    for b in range(batch):
+        d_pay[b, :plen] = torch.from_numpy(pays[b])
     d_sh = torch.full((batch, nv, ss), 0x5C, dtype=torch.uint8, device="cuda")
-    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+    E.encode_batch(nv, d_pay, plen, ps, batch, d_sh, ss)
     torch.cuda.synchronize()
     got = d_sh.cpu().numpy()
     for b in range(batch):
