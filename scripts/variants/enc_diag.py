@@ -108,7 +108,8 @@ for k in kinds:
         # line serialise in L2: ~6 ns per atomic); 1152 B of scratch
         enc = rep(enc, "launch_zero_counters(tick, sizeof(uint32_t), s)", "launch_zero_counters(tick, 1152, s)")
         extra["enc_k256.hip"] = rep(open(f"{CS}/enc_k256.hip").read(),
-                                    "return p.n == 1024 ? 256 : 0;", "return p.n == 1024 ? 1152 : 0;")
+                                    "size_t k256_scratch_bytes(const CodeParams &) { return 256; }",
+                                    "size_t k256_scratch_bytes(const CodeParams &) { return 1152; }")
     elif k == "nbread":
         for old in ("    rsync();  // the other waves are done reading this region (last tile)\n",
                     "    rsync();  // systematic rows read out of the regions\n",
