@@ -149,20 +149,24 @@ def test_measure_performance():
 
 # ---------------------------------------------------------------- device batch API
 def _batch_case(nv, plen, batch, cnt_key="threshold", seed0=0, pad=0):
-    """pad=0: tight rows (generic kernels); pad>0: rows aligned to `pad` bytes (fast kernels)."""
+    """pad=0: tight rows (generic kernels); pad>0: shard rows aligned to `pad`
+    bytes and payload rows to 64 (the fast kernels, ragged lengths included:
+    with a payload pitch off 16 B every encode takes the generic kernel)."""
     import torch
     n, k, thr = E.code_params(nv)
     sl = E.shard_len(nv, plen)
     ss = (sl + pad - 1) // pad * pad if pad else sl
+    ps = (plen + 63) // 64 * 64 if pad else plen
     pay = np.stack([synth.payload(seed0 + b, plen) for b in range(batch)])
     cnt = {"threshold": thr, "k": k}[cnt_key]
     pres = np.stack([synth.present_mask(10**6 + seed0 + b, nv, cnt, n) for b in range(batch)])
-    d_pay = torch.from_numpy(pay).cuda()
+    d_pay = torch.zeros((batch, ps), dtype=torch.uint8, device="cuda")
+    d_pay[:, :plen] = torch.from_numpy(pay).cuda()
     d_sh = torch.zeros((batch, nv, ss), dtype=torch.uint8, device="cuda")
     d_pr = torch.from_numpy(pres).cuda()
     d_el = torch.zeros((batch, n), dtype=torch.int16, device="cuda")
     d_out = torch.zeros((batch, sl * k), dtype=torch.uint8, device="cuda")
-    E.encode_batch(nv, d_pay, plen, plen, batch, d_sh, ss)
+    E.encode_batch(nv, d_pay, plen, ps, batch, d_sh, ss)
     E.error_locator(nv, d_pr, batch, d_el)
     E.reconstruct_batch(nv, d_sh, sl, ss, d_pr, d_el, batch, d_out, sl * k)
     torch.cuda.synchronize()
