@@ -1,22 +1,25 @@
 // enc_kw.hip — encode for k = 2^M = 16, 32, 64, 128 (n <= 8 k: n_validators
-// 46..765, the Polkadot validator counts of today among them), two 8-wave
-// workgroups per CU.
+// 46..765, the Polkadot validator counts of today among them) and k = 256 at
+// n = 2048 (n_validators 1025..1533), two 8-wave workgroups per CU.
 //
-// encode_k256w's model (enc_k256w.hip) at small k: per piece
-// (2 k payload bytes = k symbols) IFFT_k at index 0, then FFT_k at each coset
-// k j below n_validators (encodeLow, poly_encoder.hpp:217-240), radix-8
-// register passes in tower coordinates, wave-private LDS exchanges.  A wave
-// holds NG = 512 / k byte-planar groups of 4 pieces; a group's k positions lie
-// over k / 8 lanes x 8 registers, the group index in the lane bits above.
-// Read as position bits M..7 and encode_k256w's instance bit, the group bits
-// make every layout and exchange encode_k256w's:
+// encode_k256w's model (enc_k256w.hip): per piece (2 k
+// payload bytes = k symbols) IFFT_k at index 0, then FFT_k at each coset k j
+// below n_validators (encodeLow, poly_encoder.hpp:217-240), radix-8 register
+// passes in tower coordinates, wave-private LDS exchanges.  A wave holds NG =
+// 512 / k byte-planar groups of 4 pieces; a group's k positions lie over k / 8
+// lanes x 8 registers, the group index in the lane bits above.  Read as
+// position bits M..7 and encode_k256w's instance bit, the group bits make
+// every layout and exchange encode_k256w's:
 //  * layout A: registers p0..p2 (lane part 8 q, q = lane & (k/8 - 1));
 //  * layout B: registers p3..p5 as far as they are positions (M = 4: p3 only,
 //    M = 5: p3, p4), lanes p0..p2 and p6; for M <= 6 its elements are
 //    wave-uniform;
-//  * M = 7: stage 6 in layout C's register bit 0;
-//  * every element is x < 2^(M+2) <= 512: the 32 KB compact image holds all
-//    tables, LDS 64 KB per workgroup;
+//  * M = 7: stage 6 in layout C's register bit 0; M = 8: stages 6, 7 in
+//    layout C (encode_k256w's pass C);
+//  * every element of k <= 128 is x < 2^(M+2) <= 512: the 32 KB compact image
+//    holds all tables (LDS 64 KB per workgroup); at k = 256, n = 2048 the
+//    stage-0 elements of cosets 4..7 (512..1023) come from a 10 KB per-coset
+//    extension image brought in by LDS-DMA, as in enc_k512w.hip (74 KB);
 //  * tiles of 8 NG pieces per wave (32 KB of payload), shard-row segments of
 //    64 NG bytes stored as 16 B per lane (two groups of one wave).
 #include <hip/hip_runtime.h>
@@ -468,16 +471,14 @@ __global__ void __launch_bounds__(THREADS, 4) encode_kw(const uint8_t *__restric
     uint8_t *SH = shards + b * uint64_t(nv) * sstride;
     // every store phase of this tile but possibly the last coset's takes the
     // fast path (4 stores per lane), or none does
-    const bool fast = store_fast<M>(SH, sstride, 0, nv, piece0, npieces);
-    (void)fast;
+    [[maybe_unused]] const bool fast = store_fast<M>(SH, sstride, 0, nv, piece0, npieces);
     // k = 256, n = 2048: coset j's extension image (10 x 1 KB) -> LDS, chunk i by
     // wave i % 8, issued after the previous coset's rows-staged barrier
-    const auto dma_ext = [&](uint32_t j) __attribute__((always_inline)) {
+    [[maybe_unused]] const auto dma_ext = [&](uint32_t j) __attribute__((always_inline)) {
       const uint8_t *src = eimg + (j - 4) * kEImg256Bytes + 16 * lane;
       for (uint32_t i = wave_s; i < kEImg256Bytes / 1024; i += WAVES)
         lds_dma16(EXT8 + 1024 * i, src + 1024 * i);
     };
-    (void)dma_ext;
     const auto fetch_next = [&]() __attribute__((always_inline)) {
       next = __builtin_amdgcn_readfirstlane(*slot);
       fetch(next < total ? next / tiles_pp : 0, next < total ? next % tiles_pp : tiles_pp);
