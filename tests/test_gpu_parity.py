@@ -371,7 +371,12 @@ def test_batch_systematic():
                                                  (1024, 1_000_000, 4, 3),
                                                  # k = 1024: chunks on the 3 slot streams
                                                  # share the encode's coefficient scratch
-                                                 (4096, 60001, 7, 1)])
+                                                 (4096, 60001, 7, 1),
+                                                 # the round-6 encodes (encode_kw<4>, <6>, <8>,
+                                                 # encode_k512w) on the slot streams, their
+                                                 # tile counters in the slots' scratch
+                                                 (64, 30001, 5, 2), (300, 50001, 5, 2),
+                                                 (1500, 70001, 5, 2), (3069, 100001, 4, 0)])
 def test_host_batch_roundtrip(oracle, nv, plen, batch, chunk):
     n, k, thr = E.code_params(nv)
     sl = E.shard_len(nv, plen)
