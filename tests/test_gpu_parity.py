@@ -210,6 +210,27 @@ def test_batch_vs_oracle(oracle, nv, plen, batch, pad):
         assert out[b].tobytes() == oracle.reconstruct(nv, keep)
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_batch_random_nv_aligned(oracle, seed):
+    """n_validators drawn uniformly from 2..4096 and payload lengths
+    log-uniformly from 1 B to 1.2 MB, with 64-B payload rows and 8/16/64-B
+    shard pitches (so the fast encodes and reconstructs take whatever shape
+    falls out, ragged tails included), encode + locator + reconstruct against
+    the reference at the threshold count of random shards."""
+    rng = np.random.default_rng(4321 + seed)
+    for _ in range(8):
+        nv = int(rng.integers(2, 4097))
+        plen = int(np.exp(rng.uniform(0, np.log(1_200_000))))
+        pad = int(rng.choice([8, 16, 64]))
+        pay, pres, sh, el, out = _batch_case(nv, plen, 2, seed0=100 * seed + nv, pad=pad)
+        n, k, _ = E.code_params(nv)
+        for b in range(2):
+            ref = oracle.encode(nv, pay[b].tobytes())
+            assert b"".join(ref) == sh[b].tobytes(), (nv, plen, pad, b)
+            keep = [ref[i] if pres[b][i] else None for i in range(nv)]
+            assert out[b].tobytes() == oracle.reconstruct(nv, keep), (nv, plen, pad, b)
+
+
 @pytest.mark.parametrize("nv,plen,batch,pad", [
     (1534, 70001, 3, 64), (1535, 1, 2, 16), (1536, 3 * 32768, 2, 16), (1800, 33793, 2, 8),
     (2048, 66559, 3, 64), (2049, 40001, 2, 16), (2560, 50001, 2, 64), (2561, 30001, 2, 8),
