@@ -9,11 +9,11 @@
 // passes with wave-private LDS exchanges, the closed-form derivative and the
 // FFT restricted to the k outputs, phase 5: erased outputs times E[y]).  What
 // it takes to fit 12 waves in one CU:
-//  * LDS 160 KB = a 64 KB table image + 12 x 8 KB exchange regions.  The
-//    image (DevTables::dimg) holds planes 0 and 1 of every skew slot (the
-//    subfield tables of stages >= 2 need only those) and planes 2..4 only
-//    for the slots of IFFT stages 0 (general tables) and 1 (F9), compacted:
-//    stage-0 slot 2c -> entry c, stage-1 slot 4c + 1 -> entry 512 + c.
+//  * LDS = the 32 KB element-indexed compact image (DevTables::cimg, the
+//    headline encode's; since round 6: layouts whose element kinds are
+//    register-indexed, below) + 12 x 8 KB exchange regions = 128 KB.  Until
+//    round 6 a 64 KB reduced skew-slot image (every stage-0 table in the
+//    general form, because the kinds varied across the lanes).
 //  * no staging of the received data rows in LDS: phase 5 reads its present
 //    rows y < k (8 B per lane and row) from the shards again (the gather
 //    has just read them: L2).
@@ -26,6 +26,7 @@
 #include "dec_n1024_common.hpp"
 #include "ec_device.hpp"
 #include "ec_kernels.hpp"
+#include "cimg.hpp"
 
 namespace ecamd {
 namespace {
@@ -33,136 +34,148 @@ using namespace n1024;
 constexpr int WAVES = 12;
 constexpr int THREADS = 64 * WAVES;
 constexpr int COLS = 4 * WAVES;  // shard columns per tile
-constexpr uint32_t PLANE = Tabs::kPlane;  // 16 KB: planes 0, 1 by skew slot
-constexpr uint32_t CP2 = 2 * PLANE, CP3 = CP2 + 768 * 16, CP4 = CP3 + 768 * 16;  // compact planes
-constexpr int TAB_REGION = int(CP4 + 512 * 16);
-static_assert(TAB_REGION == kDImgBytes, "the image layout (ec_kernels.hpp)");
-constexpr int LDS_BYTES = TAB_REGION + WAVES * REG_BYTES;
+constexpr int TAB_REGION = int(kCImgBytes);  // the element-indexed compact image
+static_assert(TAB_REGION % 8192 == 0, "regions 8 KB aligned: region addresses are base | rz");
+// the tile schedule's LDS word, after the regions
+constexpr uint32_t SLOT = uint32_t(TAB_REGION + WAVES * REG_BYTES);
+constexpr int LDS_BYTES = int(SLOT + 16);
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 constexpr int ROW_WORDS = COLS / 2;  // dwords of a row segment (96 B)
-// the tile schedule's LDS word: skew slot 1023 of plane 0, which no table
-// read touches (skew indices stop at 1022; sub_alias at 1019), free once the
-// image is copied
-constexpr uint32_t SLOT = tlin(1023);
 
-// a general table of IFFT stage 0 / an F9 table of stage 1: planes 0, 1 at
-// the skew slot's address s, planes 2.. at the compact entry's address c
-__device__ __forceinline__ void tab_gen(uint32_t s, uint32_t c, Tab &T) {
-  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-  const auto rd = [](uint32_t a) { return *(const __attribute__((address_space(3))) v4u *)(uintptr_t(a)); };
-  const v4u p4 = rd(CP4 + c), p3 = rd(CP3 + c), p2 = rd(CP2 + c), p1 = rd(PLANE + s), p0 = rd(s);
-  const v4u p[5] = {p0, p1, p2, p3, p4};
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    T.t[4 * q] = p[q].x;
-    T.t[4 * q + 1] = p[q].y;
-    T.t[4 * q + 2] = p[q].z;
-    T.t[4 * q + 3] = p[q].w;
-  }
-}
-__device__ __forceinline__ void tab_f9(uint32_t s, uint32_t c, F9Tab &T) {
-  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-  const auto rd = [](uint32_t a) { return *(const __attribute__((address_space(3))) v4u *)(uintptr_t(a)); };
-  const v4u p3 = rd(CP3 + c), p2 = rd(CP2 + c), p1 = rd(PLANE + s), p0 = rd(s);
-  const v4u p[4] = {p0, p1, p2, p3};
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    T.t[4 * q] = p[q].x;
-    T.t[4 * q + 1] = p[q].y;
-    T.t[4 * q + 2] = p[q].z;
-    T.t[4 * q + 3] = p[q].w;
-  }
+// Region address of position v (8-byte cells, GF(2)-linear): conflict-free
+// for the reads (2 x 32 lanes) and writes (4 x 16 lanes) of the three layouts
+// below (scripts/search_raddr.py's condition; raddr, dec_n1024_common.hpp,
+// is 2-way on layout A' reads)
+__host__ __device__ constexpr uint32_t rz(uint32_t v) {
+  return ((v >> 5) << 8) | (((v ^ (v >> 4) ^ (v >> 5)) & 31) << 3);
 }
 
-// A radix-16 inverse pass (position bits B0..B0+3 in registers) whose 15
-// tables run through a ring of R slots: table k is requested R - 1 tables
-// ahead of its use.  Table k: stage tk(k), block bk(k) (8 + 4 + 2 + 1).  A
-// slot holds a general table (20 words), an F9 table (16) or a subfield one
-// (5); only the words a table uses are live.  At stage 0 each table feeds one
-// butterfly (~90 issue cycles), so one table ahead leaves the LDS latency
-// under 12 waves exposed.
+// The IFFT's three register layouts (lane bits / register bits -> position bits):
+//  A' lane = p2..p7, r = (p0, p1, p8, p9): stages 0, 1.  The element of a
+//     butterfly, x = pos >> (m + 1) (its table: the compact image entry x,
+//     cimg.hpp), has its kind bits (x >= 128: F9, x >= 256: general) in p8,
+//     p9, i.e. in the register index: every multiply takes the cheapest form
+//     its element allows (stage 0: 2 subfield + 2 F9 + 4 general per lane,
+//     stage 1: 4 subfield + 4 F9), where the round-5 layout (p0..p3 in
+//     registers) had p8, p9 in the lane and used the general form for all of
+//     stage 0 and the F9 form for all of stage 1.
+//  B' lane = (p0, p1, p6..p9), r = p2..p5: stages 2-5 (subfield).
+//  C  lane = p0..p5, r = (p8, p9, p6, p7): stages 6-9, every element
+//     wave-uniform (x = 0: b ^= a only), then the derivative and the FFT.
+__device__ __forceinline__ uint32_t posA2_reg(int r) { return uint32_t(r & 3) | (uint32_t(r >> 2) << 8); }
+__device__ __forceinline__ uint32_t posB2_lane(uint32_t lane) { return (lane & 3) | ((lane >> 2) << 6); }
+__device__ __forceinline__ uint32_t posC_reg(int r) {
+  return (uint32_t((r >> 2) & 3) << 6) | (uint32_t(r & 3) << 8);
+}
+
+// IFFT stages 0 and 1 in layout A'
+__device__ __forceinline__ void ipassA2(S16 &s, uint32_t lane) {
+  const uint32_t l0 = cimg_lin(lane << 1), l1 = cimg_lin(lane);
+  SubTab S0, S1;
+  F9Tab F0, F1;
+  Tab G0, G1;
+  // stage 0, pair (r, r + 1): x = ((r >> 1) & 1) | lane << 1 | (r >> 2) << 7
+  ctab(l0, cimg_lin(0), S0);
+  ctab(l0, cimg_lin(1), S1);
+  ctab(l0, cimg_lin(128), F0);
+  ib(s, 0, 1, S0);
+  ctab(l0, cimg_lin(129), F1);
+  ib(s, 2, 3, S1);
+  ctab(l0, cimg_lin(256), G0);
+  ib(s, 4, 5, F0);
+  ctab(l0, cimg_lin(257), G1);
+  ib(s, 6, 7, F1);
+  ib(s, 8, 9, G0);
+  ctab(l0, cimg_lin(384), G0);
+  ib(s, 10, 11, G1);
+  ctab(l0, cimg_lin(385), G1);
+  ctab(l1, cimg_lin(0), S0);
+  ib(s, 12, 13, G0);
+  ctab(l1, cimg_lin(64), S1);
+  ib(s, 14, 15, G1);
+  // stage 1, pair (r, r + 2): x = lane | (r >> 2) << 6
+  ctab(l1, cimg_lin(128), F0);
+  ib(s, 0, 2, S0);
+  ib(s, 1, 3, S0);
+  ctab(l1, cimg_lin(192), F1);
+  ib(s, 4, 6, S1);
+  ib(s, 5, 7, S1);
+  ib(s, 8, 10, F0);
+  ib(s, 9, 11, F0);
+  ib(s, 12, 14, F1);
+  ib(s, 13, 15, F1);
+}
+
+// IFFT stages 2-5 in layout B': radix 16 over r = p2..p5, 15 subfield tables
+// (stage 2 + t, block blk: x = lane part >> (3 + t) | blk >> (1 + t)) through
+// a ring of R slots, table k requested R - 1 tables ahead of its use
 constexpr int tk(int k) { return k < 8 ? 0 : k < 12 ? 1 : k < 14 ? 2 : 3; }
 constexpr int bk(int k) { return k < 8 ? 2 * k : k < 12 ? 4 * (k - 8) : k < 14 ? 8 * (k - 12) : 0; }
-
-// table-ring depths of passes A and B (2 / 3: 2-2, 3-5 and 4-7 were within
-// noise, profiles/r05/NOTES.md; A/B variants: scripts/variants/n1024x_knobs.py)
-constexpr int RING_A = 2, RING_B = 3;
-
-// kind of a stage's table: 0 general, 1 F9, 2 subfield
-template <int B0, int T>
-constexpr int kind_of() { return B0 + T >= SUB ? 2 : (kF9 && B0 + T == 1) ? 1 : 0; }
-
-template <int KIND>
-__device__ __forceinline__ void ring_bfly(S16 &s, int a, int b, const Tab &R) {
-  if constexpr (KIND == 0) {
-    ib(s, a, b, R);
-  } else if constexpr (KIND == 1) {
-    F9Tab F;
+constexpr int RING_B = 3;
+__device__ __forceinline__ void ipassB2(S16 &s, uint32_t lane) {
+  const uint32_t ph = (lane >> 2) << 6;  // p6..p9 of the lane part
+  const uint32_t lt[4] = {cimg_lin(ph >> 3), cimg_lin(ph >> 4), cimg_lin(ph >> 5), cimg_lin(ph >> 6)};
+  SubTab ring[RING_B];
+  const auto fetch = [&](int k, SubTab &U) __attribute__((always_inline)) {
+    ctab(lt[tk(k)], cimg_lin(uint32_t(bk(k)) >> (1 + tk(k))), U);
+  };
 #pragma unroll
-    for (int i = 0; i < 16; ++i) F.t[i] = R.t[i];
-    ib(s, a, b, F);
-  } else {
-    SubTab U;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) U.t[i] = R.t[i];
-    ib(s, a, b, U);
-  }
-}
-
-// fetch(k, slot): table k into `slot` (a Tab)
-template <int B0, int R, class Fetch>
-__device__ __forceinline__ void ipass_ring(S16 &s, Fetch &&fetch) {
-  Tab ring[R];
-#pragma unroll
-  for (int k = 0; k < R - 1; ++k) fetch(k, ring[k]);
+  for (int k = 0; k < RING_B - 1; ++k) fetch(k, ring[k]);
 #pragma unroll
   for (int k = 0; k < 15; ++k) {
-    if (k + R - 1 < 15) fetch(k + R - 1, ring[(k + R - 1) % R]);
-    const int t = tk(k), blk = bk(k), d = 1 << t;
+    if (k + RING_B - 1 < 15) fetch(k + RING_B - 1, ring[(k + RING_B - 1) % RING_B]);
+    const int blk = bk(k), d = 1 << tk(k);
 #pragma unroll
-    for (int i = 0; i < d; ++i) {
-      if (t == 0) ring_bfly<kind_of<B0, 0>()>(s, blk + i, blk + i + d, ring[k % R]);
-      else if (t == 1) ring_bfly<kind_of<B0, 1>()>(s, blk + i, blk + i + d, ring[k % R]);
-      else if (t == 2) ring_bfly<kind_of<B0, 2>()>(s, blk + i, blk + i + d, ring[k % R]);
-      else ring_bfly<kind_of<B0, 3>()>(s, blk + i, blk + i + d, ring[k % R]);
-    }
+    for (int i = 0; i < d; ++i) ib(s, blk + i, blk + i + d, ring[k % RING_B]);
   }
 }
 
-// IFFT pass A (position bits 0-3 in registers, pos = 16 lane + r) on the
-// reduced image: stage 0's general and stage 1's F9 tables read as above
-// (compact entry c = pos >> 1 at stage 0, 512 + (pos >> 2) at stage 1; tlin
-// is GF(2)-linear, so each address is a per-lane part XOR a compile-time one)
-__device__ __forceinline__ void ipassA(S16 &s, uint32_t lane) {
-  const uint32_t ls = tlin(16 * lane), lc0 = tlin(8 * lane), lc1 = tlin(4 * lane) ^ tlin(512);
-  ipass_ring<0, RING_A>(s, [&](int k, Tab &T) __attribute__((always_inline)) {
-    const int t = tk(k), blk = bk(k);
-    const uint32_t a = ls ^ tlin(skew_idx(uint32_t(blk), t));
-    if (t == 0) {
-      tab_gen(a, lc0 ^ tlin(uint32_t(blk) >> 1), T);
-    } else if (t == 1) {
-      F9Tab F;
-      tab_f9(a, lc1 ^ tlin(uint32_t(blk) >> 2), F);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) T.t[i] = F.t[i];
-    } else {
-      SubTab U;
-      tab_at(nullptr, a, U);
-#pragma unroll
-      for (int i = 0; i < 5; ++i) T.t[i] = U.t[i];
-    }
-  });
+// IFFT stages 6-9 in layout C (r bit 0 = p8, 1 = p9, 2 = p6, 3 = p7): the
+// elements are wave-uniform (broadcast table reads); x = 0 is b ^= a only
+// (the skew 0xFFFF, additive_fft.hpp:110-112)
+__device__ __forceinline__ void bx(S16 &s, int a, int b) {
+  s.l[b] ^= s.l[a];
+  s.h[b] ^= s.h[a];
 }
-
-// IFFT pass B (position bits 4-7 in registers): subfield tables only
-__device__ __forceinline__ void ipassB(S16 &s, uint32_t lane) {
-  const uint32_t lb = tlin((lane >> 4) << 8);
-  ipass_ring<4, RING_B>(s, [&](int k, Tab &T) __attribute__((always_inline)) {
-    SubTab U;
-    tab_at(nullptr, lb ^ tlin(skew_idx(uint32_t(bk(k)) << 4, 4 + tk(k))), U);
+__device__ __forceinline__ void ipassC2(S16 &s) {
+  SubTab X1, X2, X3, X4;
+  ctab(0u, cimg_lin(1), X1);
+  ctab(0u, cimg_lin(2), X2);
+  ctab(0u, cimg_lin(3), X3);
+  ctab(0u, cimg_lin(4), X4);
+  // stage 6, pair (r, r | 4): x = p7 | p8 << 1 | p9 << 2
+  bx(s, 0, 4);
+  ib(s, 8, 12, X1);
+  ib(s, 1, 5, X2);
+  ib(s, 9, 13, X3);
+  ib(s, 2, 6, X4);
+  ctab(0u, cimg_lin(5), X4);
+  ib(s, 10, 14, X4);
+  ctab(0u, cimg_lin(6), X4);
+  ib(s, 3, 7, X4);
+  ctab(0u, cimg_lin(7), X4);
+  ib(s, 11, 15, X4);
+  // stage 7, pair (r, r | 8): x = p8 | p9 << 1
+  bx(s, 0, 8);
+  bx(s, 4, 12);
+  ib(s, 1, 9, X1);
+  ib(s, 5, 13, X1);
+  ib(s, 2, 10, X2);
+  ib(s, 6, 14, X2);
+  ib(s, 3, 11, X3);
+  ib(s, 7, 15, X3);
+  // stage 8, pair (r, r | 1): x = p9
 #pragma unroll
-    for (int i = 0; i < 5; ++i) T.t[i] = U.t[i];
-  });
+  for (int q = 0; q < 4; ++q) {
+    bx(s, 4 * q, 4 * q + 1);
+    ib(s, 4 * q + 2, 4 * q + 3, X1);
+  }
+  // stage 9, pair (r, r | 2): x = 0
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    bx(s, 4 * q, 4 * q + 2);
+    bx(s, 4 * q + 1, 4 * q + 3);
+  }
 }
 
 // bytes [0, avail) (avail < 96) of a 16-B aligned row slice into w[24], zero
@@ -200,7 +213,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
   if (tid0 == 0) taken = gridDim.x + atomicAdd(tick, 1u);
   uint8_t *my = regions + wave * REG_BYTES;
 
-  // the 64 KB image (DevTables::dimg), every load issued before the first store
+  // the 32 KB compact image (DevTables::cimg), every load issued before the first store
   {
     constexpr int kPer = (TAB_REGION / 16 + THREADS - 1) / THREADS;
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -208,7 +221,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint32_t i = tid0 + k * THREADS;
-      if (i < uint32_t(TAB_REGION / 16)) v[k] = reinterpret_cast<const v4u *>(t.dimg)[i];
+      if (i < uint32_t(TAB_REGION / 16)) v[k] = reinterpret_cast<const v4u *>(t.cimg)[i];
     }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
@@ -304,7 +317,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
         }
 #pragma unroll
         for (int g = 0; g < WAVES; ++g)
-          *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + raddr(v)) = make_uint2(l[g], h[g]);
+          *reinterpret_cast<uint2 *>(regions + g * REG_BYTES + rz(v)) = make_uint2(l[g], h[g]);
       }
     }
     if (nxt < total) load_meta(nxt / tiles_pp, tid, meta_next);
@@ -342,62 +355,44 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
     load_rv();
 
     S16 s;
-    // ---- phase 2: IFFT_1024 on this wave's group
-    {  // layout A: v = 16*lane + r
-      const uint32_t la = lds_addr(my) | raddr(16 * lane);
+    // ---- phase 2: IFFT_1024 on this wave's group: layouts A', B', C (above)
+    {
+      const uint32_t la = lds_addr(my) | rz(lane << 2);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const uint2 x = lds_ld2(la ^ raddr(r));
+        const uint2 x = lds_ld2(la ^ rz(posA2_reg(r)));
         s.l[r] = x.x;
         s.h[r] = x.y;
       }
-      ipassA(s, lane);
+      ipassA2(s, lane);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) lds_st2(la ^ raddr(r), make_uint2(s.l[r], s.h[r]));
+      for (int r = 0; r < 16; ++r) lds_st2(la ^ rz(posA2_reg(r)), make_uint2(s.l[r], s.h[r]));
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
-    const uint32_t baseB = (lane & 15) | ((lane >> 4) << 8);  // layout B: bits 4-7 in registers
     {
-      const uint32_t lb = lds_addr(my) | raddr(baseB);
+      const uint32_t lb = lds_addr(my) | rz(posB2_lane(lane));
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const uint2 x = lds_ld2(lb ^ raddr(uint32_t(r) << 4));
+        const uint2 x = lds_ld2(lb ^ rz(uint32_t(r) << 2));
         s.l[r] = x.x;
         s.h[r] = x.y;
       }
-      ipassB(s, lane);  // stages 4-7: subfield (planes 0, 1)
+      ipassB2(s, lane);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) lds_st2(lb ^ raddr(uint32_t(r) << 4), make_uint2(s.l[r], s.h[r]));
+      for (int r = 0; r < 16; ++r) lds_st2(lb ^ rz(uint32_t(r) << 2), make_uint2(s.l[r], s.h[r]));
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
     // layout C: r bit0 = p8, bit1 = p9, bit2 = p6, bit3 = p7; lane = p0..p5
-    const uint32_t lc = lds_addr(my) | raddr(lane);
+    const uint32_t lc = lds_addr(my) | rz(lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const uint2 x = lds_ld2(lc ^ raddr((uint32_t((r >> 2) & 3) << 6) | (uint32_t(r & 3) << 8)));
+      const uint2 x = lds_ld2(lc ^ rz(posC_reg(r)));
       s.l[r] = x.x;
       s.h[r] = x.y;
     }
-    // IFFT stages 8 and 9 (index 0): stage 9 is b ^= a only, stage 8
-    // multiplies in its p9 = 1 block only (dec_n1024.hip)
-    {
-      SubTab Tb;
-      tab_at(nullptr, tlin(skew_idx(1u << 9, 8)), Tb);
-#pragma unroll
-      for (int hi = 0; hi < 4; ++hi) {
-        s.l[4 * hi + 1] ^= s.l[4 * hi];
-        s.h[4 * hi + 1] ^= s.h[4 * hi];
-      }
-#pragma unroll
-      for (int hi = 0; hi < 4; ++hi) ib(s, 4 * hi + 2, 4 * hi + 3, Tb);
-#pragma unroll
-      for (int hi = 0; hi < 4; ++hi) {
-        s.l[4 * hi + 2] ^= s.l[4 * hi];
-        s.h[4 * hi + 2] ^= s.h[4 * hi];
-      }
-    }
+    ipassC2(s);
 
     // phase-5 operands requested now, consumed after the derivative and the
     // FFT: E[y] of this lane's erased output rows y = 4 lane + q (and the
@@ -451,19 +446,19 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
       const uint32_t hi67 = ((lane >> 4) & 3) << 6, lo = lane & 15;
       const uint32_t hi47 = ((lane >> 2) & 15) << 4, lo01 = lane & 3;
       const uint32_t hi27 = lane << 2;
+      // the restricted FFT's elements x = pos >> (m + 1) (compact image entries)
       auto L = [&](int i) -> uint32_t {
         switch (i) {
-          case 2: return tlin(skew_idx(1u << 7, 6));
-          case 3: return tlin(skew_idx(hi67 | lo, 5));
-          case 4: return tlin(skew_idx(hi67 | lo, 4));
-          case 5: return tlin(skew_idx(hi67 | 32u | lo, 4));
-          case 6: return tlin(skew_idx(hi47 | lo01, 3));
-          case 7: return tlin(skew_idx(hi47 | lo01, 2));
-          case 8: return tlin(skew_idx(hi47 | 8u | lo01, 2));
-          // stages 1, 0: the stage-2 slot of the same (subfield) skew element
-          case 9: return tlin(sub_alias(hi27, 1));
-          case 10: return tlin(sub_alias(hi27, 0));
-          default: return tlin(sub_alias(hi27 | 2u, 0));
+          case 2: return cimg_lin(1);                         // stage 6, p7 = 1
+          case 3: return cimg_lin((hi67 | lo) >> 6);          // stage 5
+          case 4: return cimg_lin((hi67 | lo) >> 5);          // stage 4
+          case 5: return cimg_lin((hi67 | 32u | lo) >> 5);
+          case 6: return cimg_lin((hi47 | lo01) >> 4);        // stage 3
+          case 7: return cimg_lin((hi47 | lo01) >> 3);        // stage 2
+          case 8: return cimg_lin((hi47 | 8u | lo01) >> 3);
+          case 9: return cimg_lin(hi27 >> 2);                 // stage 1
+          case 10: return cimg_lin(hi27 >> 1);                // stage 0
+          default: return cimg_lin((hi27 | 2u) >> 1);
         }
       };
       const auto fx = [&](int a, int bb) {
@@ -471,13 +466,13 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
         qh[bb] ^= qh[a];
       };
       SubTab T[2];
-      tab_at(nullptr, L(2), T[0]);
-      tab_at(nullptr, L(3), T[1]);
+      ctab(0u, L(2), T[0]);
+      ctab(0u, L(3), T[1]);
       fx(0, 2);  // stage 7
       fx(1, 3);
       fx(0, 1);  // stage 6
       fb(2, 3, T[0]);
-      tab_at(nullptr, L(4), T[0]);
+      ctab(0u, L(4), T[0]);
       swap_bit(ql[0], ql[1], 4, false);
       swap_bit(qh[0], qh[1], 4, false);
       swap_bit(ql[2], ql[3], 4, false);
@@ -488,11 +483,11 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
       swap_bit(qh[1], qh[3], 5, false);
       fb(0, 2, T[1]);  // stage 5
       fb(1, 3, T[1]);
-      tab_at(nullptr, L(5), T[1]);
+      ctab(0u, L(5), T[1]);
       fb(0, 1, T[0]);  // stage 4
-      tab_at(nullptr, L(6), T[0]);
+      ctab(0u, L(6), T[0]);
       fb(2, 3, T[1]);
-      tab_at(nullptr, L(7), T[1]);
+      ctab(0u, L(7), T[1]);
       const bool l2 = (lane >> 2) & 1, l3 = (lane >> 3) & 1;
       swap_bit(ql[0], ql[1], 2, l2);
       swap_bit(qh[0], qh[1], 2, l2);
@@ -504,11 +499,11 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
       swap_bit(qh[1], qh[3], 3, l3);
       fb(0, 2, T[0]);  // stage 3
       fb(1, 3, T[0]);
-      tab_at(nullptr, L(8), T[0]);
+      ctab(0u, L(8), T[0]);
       fb(0, 1, T[1]);  // stage 2
-      tab_at(nullptr, L(9), T[1]);
+      ctab(0u, L(9), T[1]);
       fb(2, 3, T[0]);
-      tab_at(nullptr, L(10), T[0]);
+      ctab(0u, L(10), T[0]);
       const bool l0 = lane & 1, l1 = (lane >> 1) & 1;
       swap_bit(ql[0], ql[1], 0, l0);
       swap_bit(qh[0], qh[1], 0, l0);
@@ -520,7 +515,7 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
       swap_bit(qh[1], qh[3], 1, l1);
       fb(0, 2, T[1]);  // stage 1
       fb(1, 3, T[1]);
-      tab_at(nullptr, L(11), T[1]);
+      ctab(0u, L(11), T[1]);
       fb(0, 1, T[0]);  // stage 0
       fb(2, 3, T[1]);
     }
@@ -571,7 +566,7 @@ hipError_t launch_reconstruct_n1024x(const CodeParams &p, const DevTables &t,
                                      const uint32_t *d_pattern, size_t batch, uint8_t *d_out,
                                      size_t ostride, void *scratch, hipStream_t s) {
   int cus = 0;
-  if (!t.dimg || !scratch || slen / 2 < size_t(COLS)) return hipErrorInvalidValue;
+  if (!t.cimg || !scratch || slen / 2 < size_t(COLS)) return hipErrorInvalidValue;
   if (const hipError_t e = prepare_kernel(reinterpret_cast<const void *>(&reconstruct_n1024x), LDS_BYTES, &cus);
       e != hipSuccess)
     return e;
