@@ -14,9 +14,11 @@
 //    register-indexed, below) + 12 x 8 KB exchange regions = 128 KB.  Until
 //    round 6 a 64 KB reduced skew-slot image (every stage-0 table in the
 //    general form, because the kinds varied across the lanes).
-//  * no staging of the received data rows in LDS: phase 5 reads its present
-//    rows y < k (8 B per lane and row) from the shards again (the gather
-//    has just read them: L2).
+//  * phase 5's received data rows y < k: the gather copies each present
+//    row's raw 96-B segment into LDS beside the regions (24 KB of the 32 KB
+//    the compact image freed; until round 6 they were re-read from the
+//    shards into registers held across the IFFT: 10.58 -> 10.54 ms at
+//    nv = 1024, 10.23 -> 10.12 at nv = 800, profiles/r06/ab/rec_stage/).
 //  * <= 168 VGPRs: the output tables E[y] are requested after IFFT pass C,
 //    not before the transform.
 // Tile = 48 shard columns (12 waves x 4); 1 MB at n_validators 1024 is 1954
@@ -37,7 +39,12 @@ constexpr int COLS = 4 * WAVES;  // shard columns per tile
 constexpr int TAB_REGION = int(kCImgBytes);  // the element-indexed compact image
 static_assert(TAB_REGION % 8192 == 0, "regions 8 KB aligned: region addresses are base | rz");
 // the tile schedule's LDS word, after the regions
-constexpr uint32_t SLOT = uint32_t(TAB_REGION + WAVES * REG_BYTES);
+// phase 5's received rows y < 256: row slot (y & 3) << 6 | y >> 2 at a 112-B
+// pitch, so that its reads (y = 4 lane + q) are at most 2-way
+constexpr uint32_t STG = uint32_t(TAB_REGION + WAVES * REG_BYTES);
+constexpr uint32_t STG_PITCH = 112;
+__device__ __forceinline__ uint32_t stg_row(uint32_t y) { return STG + (((y & 3) << 6) | (y >> 2)) * STG_PITCH; }
+constexpr uint32_t SLOT = STG + 256 * STG_PITCH;
 constexpr int LDS_BYTES = int(SLOT + 16);
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 constexpr int ROW_WORDS = COLS / 2;  // dwords of a row segment (96 B)
@@ -308,6 +315,12 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
 #pragma unroll
         for (int g = 0; g < WAVES; ++g) l[g] = h[g] = 0;
         if (on) {  // one divergent branch for the 12 groups
+          if (v < uint32_t(K)) {  // phase 5's copy of a received data row
+#pragma unroll
+            for (int j = 0; j < ROW_WORDS / 4; ++j)
+              *reinterpret_cast<__attribute__((address_space(3))) v4u *>(uintptr_t(stg_row(v) + 16 * j)) =
+                  v4u{w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]};
+          }
 #pragma unroll
           for (int g = 0; g < WAVES; ++g) {  // columns 4g..4g+3: words (h0 l0 h1 l1)(h2 l2 h3 l3)
             const uint32_t a = w[2 * g], c = w[2 * g + 1];
@@ -331,28 +344,6 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
       cur = nxt;
       continue;
     }
-
-    // phase 5's received rows y = 4 lane + q < 256 (8 B of the row: this
-    // group's 4 columns), re-read from the shards (L2: the gather has just
-    // read them; no LDS left to stage them), requested before the IFFT
-    // (10.68 / 10.92 ms at B = 4096 with 154 VGPRs, against 10.76 / 11.00
-    // requested after it; profiles/r05/NOTES.md)
-    uint2 rv[4];
-    const auto load_rv = [&]() __attribute__((always_inline)) {
-      uint32_t ol2 = lane;
-      asm volatile("" : "+v"(ol2));
-      const bool whole = cbase + 4 <= ncols;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t m = (meta[2 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
-        rv[q] = make_uint2(0, 0);
-        if (m == 0xFFFFu) {
-          const uint8_t *row = SH + uint64_t(4 * ol2 + q) * sstride + 2 * cbase;
-          rv[q] = whole ? *reinterpret_cast<const uint2 *>(row) : load8_any(row, uint32_t(2 * (ncols - cbase)));
-        }
-      }
-    };
-    load_rv();
 
     S16 s;
     // ---- phase 2: IFFT_1024 on this wave's group: layouts A', B', C (above)
@@ -531,8 +522,9 @@ __global__ void __launch_bounds__(THREADS) reconstruct_n1024x(
         if (m != 0xFFFFu) {
           mul_acc(ql[q], qh[q], T5[q], ol[q], oh[q]);
         } else {
-          oh[q] = vperm(rv[q].y, rv[q].x, 0x06040200u);
-          ol[q] = vperm(rv[q].y, rv[q].x, 0x07050301u);
+          const uint2 rv = lds_ld2(stg_row(4 * lane + uint32_t(q)) + 8 * wave_s);
+          oh[q] = vperm(rv.y, rv.x, 0x06040200u);
+          ol[q] = vperm(rv.y, rv.x, 0x07050301u);
         }
       }
 #pragma unroll

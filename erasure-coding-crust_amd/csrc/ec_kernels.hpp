@@ -67,14 +67,6 @@ constexpr uint32_t kEImg512Stage[3] = {0, 20480, 30720};
 // j = 4..7 (elements 128 j + e, e < 128), plane q at q * 2048 + cimg_lin(e).
 constexpr uint32_t kEImg256Bytes = 10240, kEImg256Cosets = 4;
 
-// Reduced F9 image 0 (reconstruct_n1024x, 12 waves per CU): planes 0 and 1 of
-// every slot as in the F9 image (kind 0) at 0 / 16384 (the subfield tables of
-// stages >= 2 use only those), planes 2, 3 of the stage-0 (general) and
-// stage-1 (F9) slots compacted at 32768 / 45056 (slot 2c -> entry c, slot
-// 4c + 1 -> entry 512 + c; entry e at tlin(e) = cimg_lin(e)) and plane 4 of
-// the stage-0 slots at 57344: 64 KB instead of 80.
-constexpr uint32_t kDImgBytes = 65536;
-
 struct DevTables {
   const uint16_t *skews = nullptr;     // 65535
   const MulTab *mtab = nullptr;        // 65536
@@ -85,7 +77,6 @@ struct DevTables {
   const uint8_t *timg_f9 = nullptr;    // kF9Images x kTabImageBytes, F9 variants of tower image 0
   const uint8_t *cimg = nullptr;       // kCImgBytes, the element-indexed compact image
   const MulTab *mslot = nullptr;       // 65535, mslot[i] = mtab[skews[i]]: by skew slot, one load
-  const uint8_t *dimg = nullptr;       // kDImgBytes, the reduced F9 image 0
   const uint8_t *eimg512 = nullptr;    // kEImg512Cosets x kEImg512Bytes, the k = 512 encode's coset images
   const uint8_t *eimg256 = nullptr;    // kEImg256Cosets x kEImg256Bytes, the k = 256 / n = 2048 encode's
 };

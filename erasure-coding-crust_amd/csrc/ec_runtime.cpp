@@ -23,7 +23,6 @@ struct DeviceState {
   uint8_t *timg_t = nullptr;
   uint8_t *timg_f9 = nullptr;
   uint8_t *cimg = nullptr;
-  uint8_t *dimg = nullptr;
   uint8_t *eimg512 = nullptr;
   uint8_t *eimg256 = nullptr;
   MulTab *mslot = nullptr;  // mtab by skew slot (DevTables::mslot)
@@ -185,18 +184,6 @@ DeviceState *device_state() {
       !hip_ok(hipMemcpy(st->eimg512, eimg.data(), eimg.size(), hipMemcpyHostToDevice),
               "upload k512 coset images"))
     return nullptr;
-  // the reduced F9 image 0 (ec_kernels.hpp kDImgBytes) from F9 image kind 0
-  std::vector<uint8_t> dimg(kDImgBytes, 0);
-  std::memcpy(dimg.data(), img_f9.data(), 2 * 16384);
-  for (uint32_t e = 0; e < 768; ++e) {
-    const uint32_t i = e < 512 ? 2 * e : 4 * (e - 512) + 1;  // its skew slot
-    const uint32_t planes = e < 512 ? 5 : 4;
-    for (uint32_t plane = 2; plane < planes; ++plane)
-      std::memcpy(&dimg[32768 + (plane - 2) * 12288 + cimg_lin(e)], &img_f9[plane * 16384 + cimg_lin(i)], 16);
-  }
-  if (!hip_ok(hipMalloc(&st->dimg, dimg.size()), "hipMalloc(reduced image)") ||
-      !hip_ok(hipMemcpy(st->dimg, dimg.data(), dimg.size(), hipMemcpyHostToDevice), "upload reduced image"))
-    return nullptr;
   if (!hip_ok(hipMalloc(&st->timg_f9, img_f9.size()), "hipMalloc(F9 images)") ||
       !hip_ok(hipMemcpy(st->timg_f9, img_f9.data(), img_f9.size(), hipMemcpyHostToDevice),
               "upload F9 images"))
@@ -248,7 +235,6 @@ DevTables device_tables(DeviceState *d) {
   t.timg_f9 = d->timg_f9;
   t.cimg = d->cimg;
   t.mslot = d->mslot;
-  t.dimg = d->dimg;
   t.eimg512 = d->eimg512;
   t.eimg256 = d->eimg256;
   return t;

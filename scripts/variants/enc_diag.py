@@ -29,7 +29,7 @@ that work costs in the real interleaving:
     dnoout  reconstruct_n1024: the output stores dropped (values asm-consumed)
     xnobar, xnogat, xnoout  the same three for reconstruct_n1024x (writes
             OUTDIR/dec_n1024x.hip)
-    xnorv   reconstruct_n1024x: phase 5's re-read of the present rows dropped
+    xnorv   reconstruct_n1024x: phase 5's read of the staged present rows dropped
     xwdyn   reconstruct_n1024x: every wave takes its own tiles (its 4-column
             group) from a counter of its own (one 128-B line each): with
             xnobar / xnogat the waves stay balanced and the timing valid
@@ -161,8 +161,8 @@ for k in kinds:
         decx = rep(decx, "        if (on) {  // one divergent branch", "        if (meta[half] == 0x12345678u) {  //")
         extra["dec_n1024x.hip"] = decx
     elif k == "xnorv":
-        decx = rep(decx, "          rv[q] = whole ? *reinterpret_cast<const uint2 *>(row) : load8_any(row, uint32_t(2 * (ncols - cbase)));\n",
-                   "          rv[q] = make_uint2(uint32_t(reinterpret_cast<uintptr_t>(row)), q);\n")
+        decx = rep(decx, "          const uint2 rv = lds_ld2(stg_row(4 * lane + uint32_t(q)) + 8 * wave_s);\n",
+                   "          const uint2 rv = make_uint2(lane, uint32_t(q));\n")
         extra["dec_n1024x.hip"] = decx
     elif k == "xwdyn":
         W = "(tid0 & 63) == 0"

@@ -3,9 +3,8 @@
 product source; results in profiles/r05/NOTES.md):
 
   n1024x_knobs.py KNOB=VALUE[,KNOB=VALUE...] OUT.hip
-    RA=N, RB=N   table-ring depth of IFFT pass A / pass B (product: 2 / 3)
-    RVLATE=1     phase 5's re-reads requested after IFFT pass C instead of
-                 before the IFFT (product: before)
+    RB=N         table-ring depth of IFFT pass B' (product: 3; pass A' has no
+                 ring since round 6's relayout)
     PRIO=1|2     issue priority by transform phase: 1 lets waves 8-11 lead
                  pass A, 4-7 pass B, 0-3 pass C and the FFT; 2 the reverse
                  (product: equal priority)
@@ -24,12 +23,8 @@ def rep(s, old, new):
     return s.replace(old, new, 1)
 
 
-if "RA" in knobs or "RB" in knobs:
-    s = rep(s, "constexpr int RING_A = 2, RING_B = 3;",
-            f"constexpr int RING_A = {knobs.get('RA', 2)}, RING_B = {knobs.get('RB', 3)};")
-if knobs.get("RVLATE") == "1":
-    s = rep(s, "    load_rv();\n\n    S16 s;", "\n    S16 s;")
-    s = rep(s, "    // ---- phases 3 + 4:", "    load_rv();\n\n    // ---- phases 3 + 4:")
+if "RB" in knobs:
+    s = rep(s, "constexpr int RING_B = 3;", f"constexpr int RING_B = {knobs['RB']};")
 if knobs.get("PRIO") in ("1", "2"):
     lead = "2u - uint32_t(phase)" if knobs["PRIO"] == "1" else "uint32_t(phase)"
     s = rep(s, "}  // namespace\n\n__global__",
@@ -37,8 +32,8 @@ if knobs.get("PRIO") in ("1", "2"):
             f"  const uint32_t lead = {lead};\n"
             "  if (phase < 3 && (wave_s >> 2) == lead) __builtin_amdgcn_s_setprio(2);\n"
             "  else __builtin_amdgcn_s_setprio(0);\n}\n\n}  // namespace\n\n__global__")
-    s = rep(s, "      ipassA(s, lane);", "      prio3(wave_s, 0);\n      ipassA(s, lane);")
-    s = rep(s, "      ipassB(s, lane);", "      prio3(wave_s, 1);\n      ipassB(s, lane);")
+    s = rep(s, "      ipassA2(s, lane);", "      prio3(wave_s, 0);\n      ipassA2(s, lane);")
+    s = rep(s, "      ipassB2(s, lane);", "      prio3(wave_s, 1);\n      ipassB2(s, lane);")
     s = rep(s, "    // layout C: r bit0", "    prio3(wave_s, 2);\n    // layout C: r bit0")
     s = rep(s, "    // ---- phase 5: y = 4*lane", "    prio3(wave_s, 3);\n    // ---- phase 5: y = 4*lane")
 open(out, "w").write(s)

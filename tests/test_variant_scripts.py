@@ -38,7 +38,7 @@ def test_product_sources_have_no_diag_switches():
         assert "g_stamp" not in text and "ECCR_DIAG" not in text, f
 
 
-@pytest.mark.parametrize("knobs", ["RA=3,RB=5", "RVLATE=1", "PRIO=1", "PRIO=2", "RA=4,RB=7,RVLATE=1,PRIO=2"])
+@pytest.mark.parametrize("knobs", ["RB=5", "PRIO=1", "PRIO=2", "RB=7,PRIO=2"])
 def test_n1024x_knob_variant_applies(knobs, tmp_path):
     """reconstruct_n1024x's tuning switches live in
     scripts/variants/n1024x_knobs.py, not in the product source."""
