@@ -3,7 +3,7 @@
 # then an in-process A/B against the previous kernel (lib/n1024x_old.so).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r6rec; mkdir -p $O
+O=${O:-gpurun_out/r6rec}; mkdir -p $O
 stop_on_fault() { if [ "$1" -ge 124 ]; then echo "FAULT status $1 in $2: stopping"; exit "$1"; fi; }
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; tail -2 $O/pytest_gpu.log; [ $rc -ne 0 ] && grep -E "^(FAILED|ERROR)|Error|assert" $O/pytest_gpu.log | head -20
